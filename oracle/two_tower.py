@@ -1,0 +1,413 @@
+"""CPU oracle for the CEOFirmMatcher two-tower training hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product path (the
+``ceo_firm_matching`` package under ``ceo-recommender_amd/`` or its HIP
+extension) imports, links or executes this module.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg use it, and
+only as the checker / the timed CPU baseline.
+
+What it is: an explicit restatement (plain torch CPU tensor ops, any dtype,
+hand-written backward -- no autograd) of the reference algorithm:
+
+* forward           -- ``ceo_firm_matching/model.py:67-89`` (embedding gather
+                       + concat ``:69-76``, towers ``:37-62``, L2 normalise
+                       without eps ``:79-80``, scaled row dot ``:86-87``)
+* BatchNorm1d train/eval + running stats (torch ``native_batch_norm``
+  semantics: biased batch variance for normalisation, unbiased for the running
+  estimate, momentum 0.1, eps 1e-5) -- ``model.py:39,43,54,58``
+* Dropout(0.1) as ``x * (bernoulli(1-p) / (1-p))`` -- ``model.py:41,45,56,60``
+* weighted MSE      -- ``training.py:52``
+* backward          -- the autograd reverse of the above, written in closed
+                       form
+* Adam              -- ``training.py:32,55`` with torch 2.10's
+                       ``_single_tensor_adam`` update order (lerp / addcmul /
+                       sqrt / div / add / addcdiv)
+* epoch loop        -- ``training.py:36-62``
+
+Parity pin: ``tests/golden/*.npz`` were produced by importing the reference
+itself (``tests/golden/make_golden.py``); ``tests/test_oracle_golden.py``
+checks this restatement against every one of them.  Dropout masks are either
+injected (fixtures made with explicit masks) or regenerated with
+:func:`dropout_keep_mask`, a restatement of the HIP kernels' counter-based RNG
+(``ceo-recommender_amd/csrc/tt_common.h: tt_dropout_keep``).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+H0 = 64   # model.py:38  nn.Linear(in, 64)
+H1 = 32   # model.py:42  nn.Linear(64, 32)
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+TOWERS = ("firm", "ceo")
+
+
+# --------------------------------------------------------------------------
+# parameter naming (reference state_dict keys, model.py:24-65)
+# --------------------------------------------------------------------------
+def param_names(meta: dict) -> List[str]:
+    """Parameter names in ``CEOFirmMatcher.parameters()`` order."""
+    names = []
+    for i in range(len(meta["firm_cat_counts"])):
+        names.append(f"firm_embeddings.{i}.weight")
+    for i in range(len(meta["ceo_cat_counts"])):
+        names.append(f"ceo_embeddings.{i}.weight")
+    for t in TOWERS:
+        for layer in ("0", "1", "4", "5", "8"):
+            names.append(f"{t}_tower.{layer}.weight")
+            names.append(f"{t}_tower.{layer}.bias")
+    names.append("logit_scale")
+    return names
+
+
+def buffer_names() -> List[str]:
+    out = []
+    for t in TOWERS:
+        for layer in ("1", "5"):
+            out += [f"{t}_tower.{layer}.running_mean",
+                    f"{t}_tower.{layer}.running_var",
+                    f"{t}_tower.{layer}.num_batches_tracked"]
+    return out
+
+
+# --------------------------------------------------------------------------
+# dropout RNG restatement (HIP kernels: tt_common.h tt_dropout_keep)
+# --------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    z = z.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def dropout_key(seed: int, step: int, tower: int, layer: int) -> int:
+    """Per-(seed, step, tower, layer) stream key (tt_common.h tt_dropout_key)."""
+    k = (seed * 0x9E3779B97F4A7C15 + step * 0xD1B54A32D192ED03
+         + (tower * 2 + layer + 1) * 0x8CB92BA72F3D8DD7) & _M64
+    return int(_mix64(np.array([k], dtype=np.uint64))[0])
+
+
+def dropout_keep_mask(seed: int, step: int, tower: int, layer: int,
+                      n_rows: int, width: int, p: float) -> np.ndarray:
+    """bool[n_rows, width]: True where the element is kept (prob 1-p)."""
+    if p <= 0.0:
+        return np.ones((n_rows, width), dtype=bool)
+    key = np.uint64(dropout_key(seed, step, tower, layer))
+    ctr = np.arange(n_rows * width, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = key + ctr * np.uint64(0x9E3779B97F4A7C15)
+    h = (_mix64(z) >> np.uint64(40)).astype(np.int64)  # 24 random bits
+    thr = int(p * 16777216.0)
+    return (h >= thr).reshape(n_rows, width)
+
+
+# --------------------------------------------------------------------------
+# forward / backward
+# --------------------------------------------------------------------------
+def _tower_input(params, tower, num, cat):
+    embs = [params[f"{tower}_embeddings.{i}.weight"][cat[:, i]]
+            for i in range(cat.shape[1])]
+    return torch.cat([num] + embs, dim=1) if embs else num
+
+
+def _bn_train(z, gamma, beta, rm, rv, momentum=BN_MOMENTUM, eps=BN_EPS):
+    n = z.shape[0]
+    if n < 2:
+        raise ValueError("Expected more than 1 value per channel when training")
+    mu = z.mean(0)
+    var = ((z - mu) ** 2).mean(0)
+    invstd = 1.0 / torch.sqrt(var + eps)
+    zhat = (z - mu) * invstd
+    y = zhat * gamma + beta
+    new_rm = rm * (1 - momentum) + mu * momentum
+    new_rv = rv * (1 - momentum) + var * (n / (n - 1)) * momentum
+    return y, zhat, invstd, new_rm, new_rv
+
+
+def _bn_eval(z, gamma, beta, rm, rv, eps=BN_EPS):
+    invstd = 1.0 / torch.sqrt(rv + eps)
+    zhat = (z - rm) * invstd
+    return zhat * gamma + beta
+
+
+def dropout_scale(p: float) -> float:
+    """Float32 value of the kept-element multiplier (torch: noise.div_(1-p))."""
+    return float(np.float32(1.0) / np.float32(1.0 - p)) if p > 0 else 1.0
+
+
+def forward(params: Dict[str, torch.Tensor], buffers: Dict[str, torch.Tensor],
+            batch: Dict[str, torch.Tensor], train: bool,
+            masks: Optional[Dict[Tuple[int, int], torch.Tensor]] = None,
+            p: float = 0.1):
+    """Returns (score [B], cache, new_buffers).
+
+    ``masks[(tower, layer)]`` is a {0,1} tensor [B, H]; None means no dropout
+    (p = 0 or eval).  ``cache`` holds what the closed-form backward needs.
+    """
+    dt = params["logit_scale"].dtype
+    cache = {"towers": []}
+    newbuf = dict(buffers)
+    outs = []
+    for ti, t in enumerate(TOWERS):
+        num = batch[f"{t}_numeric"].to(dt)
+        cat = batch[f"{t}_cat"].long()
+        x = _tower_input(params, t, num, cat)
+        c = {"x": x, "cat": cat}
+        h = x
+        for li, (lin, bn) in enumerate((("0", "1"), ("4", "5"))):
+            W = params[f"{t}_tower.{lin}.weight"]
+            b = params[f"{t}_tower.{lin}.bias"]
+            z = h @ W.t() + b
+            g = params[f"{t}_tower.{bn}.weight"]
+            be = params[f"{t}_tower.{bn}.bias"]
+            rmk, rvk = f"{t}_tower.{bn}.running_mean", f"{t}_tower.{bn}.running_var"
+            if train:
+                y, zhat, invstd, nrm, nrv = _bn_train(z, g, be, buffers[rmk].to(dt), buffers[rvk].to(dt))
+                newbuf[rmk], newbuf[rvk] = nrm, nrv
+                nbk = f"{t}_tower.{bn}.num_batches_tracked"
+                newbuf[nbk] = buffers[nbk] + 1
+            else:
+                y = _bn_eval(z, g, be, buffers[rmk].to(dt), buffers[rvk].to(dt))
+                zhat, invstd = None, None
+            r = torch.clamp(y, min=0)
+            if train and masks is not None and (ti, li) in masks:
+                noise = masks[(ti, li)].to(dt) * dropout_scale(p)
+                a = r * noise
+            else:
+                noise = None
+                a = r
+            c[f"h{li}"] = h
+            c[f"y{li}"] = y
+            c[f"zhat{li}"] = zhat
+            c[f"invstd{li}"] = invstd
+            c[f"noise{li}"] = noise
+            c[f"a{li}"] = a
+            h = a
+        W8 = params[f"{t}_tower.8.weight"]
+        u = h @ W8.t() + params[f"{t}_tower.8.bias"]
+        c["u"] = u
+        cache["towers"].append(c)
+        outs.append(u)
+    u, v = outs
+    nu = u.norm(dim=1, keepdim=True)
+    nv = v.norm(dim=1, keepdim=True)
+    un, vn = u / nu, v / nv
+    s = params["logit_scale"].exp()
+    cos = (un * vn).sum(1)
+    score = cos * s
+    cache.update(nu=nu, nv=nv, un=un, vn=vn, cos=cos, s=s, score=score)
+    return score, cache, newbuf
+
+
+def weighted_mse(score, target, weight):
+    """training.py:52  loss = (w * (p - t)**2).mean(); returns (loss, dL/dscore)."""
+    target = target.reshape(-1).to(score.dtype)
+    weight = weight.reshape(-1).to(score.dtype)
+    diff = score - target
+    loss = (weight * diff ** 2).mean()
+    dscore = 2.0 * weight * diff / score.shape[0]
+    return loss, dscore
+
+
+def _bn_backward(dy, zhat, invstd, gamma):
+    n = dy.shape[0]
+    dgamma = (dy * zhat).sum(0)
+    dbeta = dy.sum(0)
+    dzhat = dy * gamma
+    dz = invstd * (dzhat - dzhat.sum(0) / n - zhat * (dzhat * zhat).sum(0) / n)
+    return dz, dgamma, dbeta
+
+
+def backward(params, cache, dscore) -> Dict[str, torch.Tensor]:
+    """Closed-form gradients of sum(dscore * score) w.r.t. every parameter."""
+    grads = {}
+    s, cos, score = cache["s"], cache["cos"], cache["score"]
+    grads["logit_scale"] = (dscore * score).sum()
+    dc = (dscore * s)[:, None]
+    un, vn, nu, nv = cache["un"], cache["vn"], cache["nu"], cache["nv"]
+    du = dc * (vn - un * cos[:, None]) / nu
+    dv = dc * (un - vn * cos[:, None]) / nv
+    for ti, (t, dout) in enumerate(zip(TOWERS, (du, dv))):
+        c = cache["towers"][ti]
+        a1 = c["a1"]
+        W8 = params[f"{t}_tower.8.weight"]
+        grads[f"{t}_tower.8.weight"] = dout.t() @ a1
+        grads[f"{t}_tower.8.bias"] = dout.sum(0)
+        da = dout @ W8
+        for li, (lin, bn) in reversed(list(enumerate((("0", "1"), ("4", "5"))))):
+            y, noise = c[f"y{li}"], c[f"noise{li}"]
+            dr = da * noise if noise is not None else da
+            dy = dr * (y > 0).to(dr.dtype)
+            dz, dg, dbe = _bn_backward(dy, c[f"zhat{li}"], c[f"invstd{li}"],
+                                       params[f"{t}_tower.{bn}.weight"])
+            grads[f"{t}_tower.{bn}.weight"] = dg
+            grads[f"{t}_tower.{bn}.bias"] = dbe
+            h = c[f"h{li}"]
+            grads[f"{t}_tower.{lin}.weight"] = dz.t() @ h
+            grads[f"{t}_tower.{lin}.bias"] = dz.sum(0)
+            da = dz @ params[f"{t}_tower.{lin}.weight"]
+        # da is now dX; scatter into the embedding tables (EmbeddingBackward)
+        cat = c["cat"]
+        n_emb = cat.shape[1]
+        if n_emb:
+            E = params[f"{t}_embeddings.0.weight"].shape[1]
+            n_num = c["x"].shape[1] - n_emb * E
+            for i in range(n_emb):
+                tab = params[f"{t}_embeddings.{i}.weight"]
+                g = torch.zeros_like(tab)
+                g.index_add_(0, cat[:, i], da[:, n_num + i * E: n_num + (i + 1) * E])
+                grads[f"{t}_embeddings.{i}.weight"] = g
+    return grads
+
+
+# --------------------------------------------------------------------------
+# Adam (torch 2.10 _single_tensor_adam, defaults betas .9/.999 eps 1e-8)
+# --------------------------------------------------------------------------
+class Adam:
+    def __init__(self, params: Dict[str, torch.Tensor], lr=4e-4,
+                 betas=(0.9, 0.999), eps=1e-8):
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+        self.m = {k: torch.zeros_like(v) for k, v in params.items()}
+        self.v = {k: torch.zeros_like(v) for k, v in params.items()}
+        self.t = 0
+
+    def step(self, params, grads):
+        self.t += 1
+        bc1 = 1 - self.b1 ** self.t
+        bc2 = 1 - self.b2 ** self.t
+        step_size = self.lr / bc1
+        bc2_sqrt = math.sqrt(bc2)
+        for k, p in params.items():
+            g = grads[k]
+            m, v = self.m[k], self.v[k]
+            m.lerp_(g, 1 - self.b1)
+            v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            denom = (v.sqrt() / bc2_sqrt).add_(self.eps)
+            p.addcdiv_(m, denom, value=-step_size)
+
+
+# --------------------------------------------------------------------------
+# step / loop helpers
+# --------------------------------------------------------------------------
+def train_step(params, buffers, opt: Adam, batch, masks=None, p=0.1):
+    """One reference training step (training.py:44-57).  Mutates params,
+    returns (loss, grads, new_buffers)."""
+    score, cache, newbuf = forward(params, buffers, batch, train=True, masks=masks, p=p)
+    loss, dscore = weighted_mse(score, batch["target"], batch["weights"])
+    grads = backward(params, cache, dscore)
+    opt.step(params, grads)
+    return loss, grads, newbuf
+
+
+def torch_dropout_masks(B: int, dtype=torch.float32, p: float = 0.1,
+                        generator: Optional[torch.Generator] = None):
+    """Bernoulli(1-p) keep masks drawn with torch's RNG (reference-speed CPU
+    baseline; not used for parity)."""
+    out = {}
+    for ti in range(2):
+        for li, H in enumerate((H0, H1)):
+            m = torch.empty(B, H, dtype=dtype)
+            m.bernoulli_(1 - p, generator=generator)
+            out[(ti, li)] = m
+    return out
+
+
+def init_params_like_reference(meta: dict, latent: int, emb_large: int = 48,
+                               emb_medium: int = 8, dtype=torch.float32,
+                               generator: Optional[torch.Generator] = None):
+    """Fresh parameters drawn in the reference's construction order
+    (model.py:24-65: Embedding N(0,1), Linear kaiming-uniform(a=sqrt5) weight
+    and U(+-1/sqrt(fan_in)) bias, BN gamma 1 beta 0, logit_scale log(1/0.07)).
+    Consumes the RNG exactly like ``CEOFirmMatcher(meta, cfg)`` does."""
+    g = generator
+    P = {}
+    for i, n in enumerate(meta["firm_cat_counts"]):
+        P[f"firm_embeddings.{i}.weight"] = torch.empty(n, emb_large).normal_(generator=g)
+    for i, n in enumerate(meta["ceo_cat_counts"]):
+        P[f"ceo_embeddings.{i}.weight"] = torch.empty(n, emb_medium).normal_(generator=g)
+    for t, n_num, ncat, E in (("firm", meta["n_firm_numeric"], len(meta["firm_cat_counts"]), emb_large),
+                              ("ceo", meta["n_ceo_numeric"], len(meta["ceo_cat_counts"]), emb_medium)):
+        d_in = n_num + ncat * E
+        for lin, bn, fin, fout in (("0", "1", d_in, H0), ("4", "5", H0, H1), ("8", None, H1, latent)):
+            bound = 1.0 / math.sqrt(fin)
+            # kaiming_uniform_(a=sqrt(5)) == U(-1/sqrt(fan_in), 1/sqrt(fan_in))
+            P[f"{t}_tower.{lin}.weight"] = torch.empty(fout, fin).uniform_(-bound, bound, generator=g)
+            P[f"{t}_tower.{lin}.bias"] = torch.empty(fout).uniform_(-bound, bound, generator=g)
+            if bn:
+                P[f"{t}_tower.{bn}.weight"] = torch.ones(fout)
+                P[f"{t}_tower.{bn}.bias"] = torch.zeros(fout)
+    P["logit_scale"] = torch.ones([]) * float(np.log(1 / 0.07))
+    order = param_names(meta)
+    return {k: P[k].to(dtype) for k in order}
+
+
+def fresh_buffers(dtype=torch.float32):
+    B = {}
+    for t in TOWERS:
+        for bn, H in (("1", H0), ("5", H1)):
+            B[f"{t}_tower.{bn}.running_mean"] = torch.zeros(H, dtype=dtype)
+            B[f"{t}_tower.{bn}.running_var"] = torch.ones(H, dtype=dtype)
+            B[f"{t}_tower.{bn}.num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+    return B
+
+
+def ddp_average_grads(params, buffers, shards: Sequence[dict], masks_per_shard=None, p=0.1):
+    """Simulated DDP: per-shard forward with LOCAL BatchNorm
+    statistics, per-shard weighted-MSE grads, averaged over shards."""
+    acc = None
+    for si, b in enumerate(shards):
+        m = masks_per_shard[si] if masks_per_shard else None
+        score, cache, _ = forward(params, buffers, b, train=True, masks=m, p=p)
+        _, dscore = weighted_mse(score, b["target"], b["weights"])
+        g = backward(params, cache, dscore)
+        if acc is None:
+            acc = {k: v.clone() for k, v in g.items()}
+        else:
+            for k in acc:
+                acc[k] += g[k]
+    return {k: v / len(shards) for k, v in acc.items()}
+
+
+# --------------------------------------------------------------------------
+# CPU baseline loop (training.py:36-62 over a CEOFirmDataset-like loader)
+# --------------------------------------------------------------------------
+class PairDataset(torch.utils.data.Dataset):
+    """Per-sample dict dataset -- restates CEOFirmDataset (data.py:180-198)."""
+
+    def __init__(self, data):
+        self.data = data
+        self.length = len(data["target"])
+
+    def __len__(self):
+        return self.length
+
+    def __getitem__(self, idx):
+        d = self.data
+        return {k: d[k][idx] for k in ("firm_numeric", "firm_cat", "ceo_numeric",
+                                       "ceo_cat", "target", "weights")}
+
+
+def cpu_train_epoch(params, buffers, opt: Adam, batches, p=0.1, max_steps=None):
+    """Runs the reference training step over ``batches`` (an iterable of batch
+    dicts) with torch-RNG dropout.  Returns (pairs, mean loss, buffers)."""
+    total, n, pairs = 0.0, 0, 0
+    for batch in batches:
+        B = batch["target"].shape[0]
+        masks = torch_dropout_masks(B, dtype=params["logit_scale"].dtype, p=p) if p > 0 else None
+        loss, _, buffers = train_step(params, buffers, opt, batch, masks=masks, p=p)
+        total += float(loss)
+        n += 1
+        pairs += B
+        if max_steps is not None and n >= max_steps:
+            break
+    return pairs, total / max(n, 1), buffers

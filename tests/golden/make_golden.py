@@ -1,0 +1,306 @@
+"""Generate the golden parity vectors from the REAL reference implementation.
+
+Run once in the build container (the only place ``/root/reference`` exists):
+
+    python tests/golden/make_golden.py
+
+It imports the reference package read-only (``shap``/``seaborn`` are stubbed:
+neither is on the hot path -- SURVEY.md 8c), runs ``CEOFirmMatcher`` /
+weighted MSE / ``torch.optim.Adam`` / ``train_model`` exactly as the
+reference does, and writes small ``.npz`` fixtures (inputs + expected
+outputs) next to this script.  Nothing here ships in the product, and no test
+imports the reference at run time: the tests read only the ``.npz`` files.
+
+Fixtures:
+  * ``<case>.npz`` for case in {meta_test, cfg2, cfg3}:
+      init params/buffers, eval forward, train forward + grads with p = 0,
+      the same with injected dropout masks (p = 0.1), fp64 grads (truth),
+      params after 1 and 5 Adam steps (p = 0, fixed batch sequence).
+  * ``ddp.npz``: per-shard local-BN grads averaged over G in {2, 4, 8}
+      shards + one Adam step (DistributedDataParallel semantics).
+  * ``cli.npz``: the default CLI pipeline (cli.py:29-59) with dropout
+      disabled and EPOCHS=6 under torch.manual_seed(1234): the transformed
+      train tensors, printed loss lines and final state_dict.
+"""
+import contextlib
+import io
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+
+for _m in ("shap", "seaborn"):
+    sys.modules.setdefault(_m, types.ModuleType(_m))
+sys.path.insert(0, REF)
+sys.dont_write_bytecode = True
+
+import ceo_firm_matching as ref  # noqa: E402
+from ceo_firm_matching.model import CEOFirmMatcher  # noqa: E402
+
+torch.set_num_threads(8)
+
+META_TEST = {"n_firm_numeric": 12, "firm_cat_counts": [4, 4, 2, 2],
+             "n_ceo_numeric": 2, "ceo_cat_counts": [2, 4, 2, 2, 2, 2, 2]}
+
+CASES = {
+    # name: (metadata, latent, batch)
+    "meta_test": (META_TEST, 60, 32),
+    "cfg2": ({"n_firm_numeric": 32, "firm_cat_counts": [], "n_ceo_numeric": 32,
+              "ceo_cat_counts": []}, 64, 256),
+    "cfg3": ({"n_firm_numeric": 64, "firm_cat_counts": [], "n_ceo_numeric": 64,
+              "ceo_cat_counts": []}, 128, 512),
+}
+
+
+class MaskDropout(torch.nn.Module):
+    """Dropout with an injected keep-mask, computed like ATen's dropout:
+    noise = mask.div_(1 - p); out = x * noise."""
+
+    def __init__(self, p):
+        super().__init__()
+        self.p = p
+        self.mask = None
+
+    def forward(self, x):
+        if not self.training or self.mask is None:
+            return x
+        noise = self.mask.to(x.dtype).div_(1 - self.p)
+        return x * noise
+
+
+def make_config(latent):
+    cfg = ref.Config()
+    cfg.LATENT_DIM = latent
+    return cfg
+
+
+def make_batch(meta, B, rng):
+    kf, kc = len(meta["firm_cat_counts"]), len(meta["ceo_cat_counts"])
+    b = {
+        "firm_numeric": rng.standard_normal((B, meta["n_firm_numeric"])).astype(np.float32),
+        "firm_cat": np.stack([rng.integers(0, n, B) for n in meta["firm_cat_counts"]], 1).astype(np.int64)
+        if kf else np.zeros((B, 0), np.int64),
+        "ceo_numeric": rng.standard_normal((B, meta["n_ceo_numeric"])).astype(np.float32),
+        "ceo_cat": np.stack([rng.integers(0, n, B) for n in meta["ceo_cat_counts"]], 1).astype(np.int64)
+        if kc else np.zeros((B, 0), np.int64),
+        "target": rng.standard_normal((B, 1)).astype(np.float32),
+    }
+    sd = rng.uniform(0.1, 1.0, (B, 1))
+    b["weights"] = (1.0 / (sd ** 2 + 1e-6)).astype(np.float32)
+    return b
+
+
+def tt(b, dtype=torch.float32):
+    out = {}
+    for k, v in b.items():
+        t = torch.from_numpy(np.ascontiguousarray(v))
+        out[k] = t.to(dtype) if t.is_floating_point() else t
+    return out
+
+
+def set_dropout(model, p=None, masks=None):
+    """p: replace every nn.Dropout's p; masks: {(tower, layer): mask} ->
+    swap the Dropout modules for MaskDropout with that mask."""
+    for ti, tower in enumerate((model.firm_tower, model.ceo_tower)):
+        for li, idx in enumerate((3, 7)):
+            if masks is not None:
+                md = MaskDropout(0.1)
+                md.mask = masks[(ti, li)]
+                tower[idx] = md
+            elif p is not None:
+                tower[idx].p = p
+
+
+def run_forward_backward(model, batch):
+    model.train()
+    model.zero_grad(set_to_none=True)
+    preds = model(batch["firm_numeric"], batch["firm_cat"], batch["ceo_numeric"], batch["ceo_cat"])
+    loss = (batch["weights"] * (preds - batch["target"]) ** 2).mean()
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    return preds.detach().clone(), loss.detach().clone(), grads
+
+
+def put(out, prefix, d):
+    for k, v in d.items():
+        out[f"{prefix}/{k}"] = v.detach().cpu().clone().numpy() if torch.is_tensor(v) else np.array(v, copy=True)
+
+
+def gen_case(name, meta, latent, B):
+    rng = np.random.default_rng({"meta_test": 1, "cfg2": 2, "cfg3": 3}[name])
+    cfg = make_config(latent)
+    torch.manual_seed(0)
+    model = CEOFirmMatcher(meta, cfg)
+    init_sd = {k: v.clone() for k, v in model.state_dict().items()}
+    out = {"meta/n_firm_numeric": meta["n_firm_numeric"], "meta/n_ceo_numeric": meta["n_ceo_numeric"],
+           "meta/firm_cat_counts": np.array(meta["firm_cat_counts"], np.int64),
+           "meta/ceo_cat_counts": np.array(meta["ceo_cat_counts"], np.int64),
+           "meta/latent": latent}
+    put(out, "init", init_sd)
+    batch_np = make_batch(meta, B, rng)
+    put(out, "batch", batch_np)
+    batch = tt(batch_np)
+
+    # eval forward (BN running stats: perturb them so eval is non-trivial)
+    with torch.no_grad():
+        for tower in (model.firm_tower, model.ceo_tower):
+            for idx in (1, 5):
+                bn = tower[idx]
+                bn.running_mean.copy_(torch.from_numpy(rng.normal(0, 0.3, bn.running_mean.shape).astype(np.float32)))
+                bn.running_var.copy_(torch.from_numpy(rng.uniform(0.5, 2.0, bn.running_var.shape).astype(np.float32)))
+    put(out, "eval_buffers", {k: v for k, v in model.state_dict().items() if "running" in k})
+    model.eval()
+    with torch.no_grad():
+        out["eval/score"] = model(batch["firm_numeric"], batch["firm_cat"], batch["ceo_numeric"], batch["ceo_cat"]).numpy()
+    model.load_state_dict(init_sd)
+
+    # train, p = 0
+    set_dropout(model, p=0.0)
+    preds, loss, grads = run_forward_backward(model, batch)
+    out["train_p0/score"] = preds.numpy()
+    out["train_p0/loss"] = loss.numpy()
+    put(out, "train_p0/grad", grads)
+    put(out, "train_p0/buffers", {k: v for k, v in model.state_dict().items() if "running" in k or "num_batches" in k})
+
+    # fp64 truth for the same step
+    m64 = CEOFirmMatcher(meta, cfg).double()
+    m64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in init_sd.items()})
+    set_dropout(m64, p=0.0)
+    preds64, loss64, grads64 = run_forward_backward(m64, tt(batch_np, torch.float64))
+    out["train_p0_f64/score"] = preds64.numpy()
+    out["train_p0_f64/loss"] = loss64.numpy()
+    put(out, "train_p0_f64/grad", grads64)
+
+    # injected dropout masks, p = 0.1
+    model.load_state_dict(init_sd)
+    masks = {}
+    for ti in range(2):
+        for li, H in enumerate((64, 32)):
+            masks[(ti, li)] = torch.from_numpy((rng.random((B, H)) >= 0.1).astype(np.float32))
+            out[f"mask/{ti}_{li}"] = masks[(ti, li)].numpy().astype(np.uint8)
+    set_dropout(model, masks=masks)
+    preds, loss, grads = run_forward_backward(model, batch)
+    out["train_mask/score"] = preds.numpy()
+    out["train_mask/loss"] = loss.numpy()
+    put(out, "train_mask/grad", grads)
+
+    # k-step Adam, p = 0, a fixed sequence of 5 batches
+    torch.manual_seed(0)
+    model = CEOFirmMatcher(meta, cfg)
+    model.load_state_dict(init_sd)
+    set_dropout(model, p=0.0)
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.LEARNING_RATE)
+    losses = []
+    for k in range(5):
+        bnp = make_batch(meta, B, rng)
+        put(out, f"steps/batch{k}", bnp)
+        b = tt(bnp)
+        model.train()
+        opt.zero_grad()
+        preds = model(b["firm_numeric"], b["firm_cat"], b["ceo_numeric"], b["ceo_cat"])
+        loss = (b["weights"] * (preds - b["target"]) ** 2).mean()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+        if k in (0, 4):
+            put(out, f"steps/after{k + 1}", model.state_dict())
+    out["steps/losses"] = np.array(losses)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(f"wrote {name}.npz ({len(out)} arrays)")
+
+
+def gen_ddp():
+    meta, latent = CASES["cfg2"][0], 64
+    cfg = make_config(latent)
+    rng = np.random.default_rng(7)
+    torch.manual_seed(0)
+    base = CEOFirmMatcher(meta, cfg)
+    init_sd = {k: v.clone() for k, v in base.state_dict().items()}
+    out = {}
+    put(out, "init", init_sd)
+    for G in (2, 4, 8):
+        Bl = 64
+        shards = [make_batch(meta, Bl, rng) for _ in range(G)]
+        acc = None
+        for s, bnp in enumerate(shards):
+            put(out, f"G{G}/shard{s}", bnp)
+            m = CEOFirmMatcher(meta, cfg)
+            m.load_state_dict(init_sd)
+            set_dropout(m, p=0.0)
+            _, _, grads = run_forward_backward(m, tt(bnp))
+            if acc is None:
+                acc = {k: v.clone() for k, v in grads.items()}
+            else:
+                for k in acc:
+                    acc[k] += grads[k]
+        avg = {k: v / G for k, v in acc.items()}
+        put(out, f"G{G}/avg_grad", avg)
+        m = CEOFirmMatcher(meta, cfg)
+        m.load_state_dict(init_sd)
+        opt = torch.optim.Adam(m.parameters(), lr=cfg.LEARNING_RATE)
+        for n, p in m.named_parameters():
+            p.grad = avg[n].clone()
+        opt.step()
+        put(out, f"G{G}/after_step", {n: p.detach() for n, p in m.named_parameters()})
+    np.savez_compressed(os.path.join(HERE, "ddp.npz"), **out)
+    print("wrote ddp.npz")
+
+
+def gen_cli():
+    """cli.py:29-59 with EPOCHS=6 and dropout disabled (p=0)."""
+    from sklearn.model_selection import train_test_split
+    from torch.utils.data import DataLoader
+    from ceo_firm_matching.data import DataProcessor, CEOFirmDataset
+    from ceo_firm_matching.synthetic import generate_synthetic_data
+    from ceo_firm_matching.training import train_model
+
+    orig_dropout = torch.nn.Dropout.__init__
+
+    def no_dropout(self, p=0.5, inplace=False):
+        orig_dropout(self, 0.0, inplace)
+
+    cfg = ref.Config()
+    cfg.EPOCHS = 6
+    cfg.DEVICE = torch.device("cpu")
+    processor = DataProcessor(cfg)
+    raw = generate_synthetic_data(1000)
+    df = processor.prepare_features(raw)
+    train_df, val_df = train_test_split(df, test_size=0.2, random_state=42)
+    processor.fit(train_df)
+    train_data = processor.transform(train_df)
+    val_data = processor.transform(val_df)
+    out = {}
+    for k in ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights"):
+        out[f"train/{k}"] = train_data[k].numpy()
+        out[f"val/{k}"] = val_data[k].numpy()
+    out["meta/firm_cat_counts"] = np.array(train_data["firm_cat_counts"], np.int64)
+    out["meta/ceo_cat_counts"] = np.array(train_data["ceo_cat_counts"], np.int64)
+    out["meta/n_firm_numeric"] = train_data["n_firm_numeric"]
+    out["meta/n_ceo_numeric"] = train_data["n_ceo_numeric"]
+    torch.nn.Dropout.__init__ = no_dropout
+    try:
+        torch.manual_seed(1234)
+        train_loader = DataLoader(CEOFirmDataset(train_data), batch_size=256, shuffle=True)
+        val_loader = DataLoader(CEOFirmDataset(val_data), batch_size=256, shuffle=False)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            model = train_model(train_loader, val_loader, train_data, cfg)
+    finally:
+        torch.nn.Dropout.__init__ = orig_dropout
+    lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("Epoch")]
+    out["printed"] = np.array(lines)
+    put(out, "final", model.state_dict())
+    np.savez_compressed(os.path.join(HERE, "cli.npz"), **out)
+    print("wrote cli.npz:", lines)
+
+
+if __name__ == "__main__":
+    for name, (meta, latent, B) in CASES.items():
+        gen_case(name, meta, latent, B)
+    gen_ddp()
+    gen_cli()

@@ -1,0 +1,315 @@
+"""Benchmark: CEOFirmMatcher training pairs/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2]
+
+A "step" is one fused training step (forward, weighted MSE, backward, Adam;
+all-reduce of the gradient when N > 1) over one batch of synthetic pairs that
+are already resident in HBM.  Default workload = BASELINE cfg 3 per GPU
+(10M pairs, 64x64 features, LATENT 128, batch 16384 per GPU) -- cfg 4 when run
+on N GPUs (weak scaling: every rank trains its own 16384-pair batches from its
+own shard of ceil(10M/N) pairs, one flat-gradient all-reduce over RCCL per
+step).  Prints ONE JSON line on rank 0.
+
+Extra legs (rank 0, N=1 only for the CPU baseline):
+* roofline : per-kernel HIP-event timing of K more steps on the launch stream;
+  the dominant kernel's algorithmic FLOP/s (or bytes/s) vs the MI355X peak;
+  HBM traffic from the committed rocprofv3 PMC summary when present.
+* cosine_roofline : the standalone fused L2-norm + cosine + weighted-MSE
+  fwd/bwd kernel over 4M pairs at D=128 (HBM-bound; BASELINE metric part 2).
+* cpu_baseline : the CPU oracle (oracle/two_tower.py, the reference algorithm
+  restated in torch CPU ops) timed on this host, reference loop (per-sample
+  Dataset + DataLoader(shuffle=True)) on a 524,288-pair sample.
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ceo-recommender_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # name: (pairs, n_firm, n_ceo, latent, batch per GPU)
+    "cfg2": (1_000_000, 32, 32, 64, 4096),
+    "cfg3": (10_000_000, 64, 64, 128, 16384),
+}
+PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_FP32_TFLOPS = 157.3     # dense fp32 (vector == MFMA f32) spec
+KERNELS = ("k_l0_fwd", "k_l4_fwd", "k_top", "k_bwd_mid", "k_bwd_first", "k_reduce_adam")
+
+
+def kernel_work(nf, nc, D, B, n_params, n_tiles):
+    """Algorithmic FLOPs and HBM bytes per launch of each step kernel
+    (both towers; FLOPs count 2 per multiply-add; bytes = compulsory
+    activation / input / partial traffic, fp32)."""
+    f = 4
+    fl = {
+        "k_l0_fwd": 2 * B * 64 * (nf + nc),
+        "k_l4_fwd": 2 * 2 * B * 32 * 64,
+        "k_top": 2 * (3 * B * D * 32) * 2,          # U,V fwd + dW8 + dA1, both towers
+        "k_bwd_mid": 2 * 2 * (2 * B * 32 * 64),     # dW4 + dA0
+        "k_bwd_first": 2 * B * 64 * (nf + nc),      # dW0
+        "k_reduce_adam": 0,
+    }
+    slab_w = lambda n: n_tiles * n * f  # noqa: E731
+    by = {
+        "k_l0_fwd": B * (nf + nc) * f + 2 * B * 64 * f,
+        "k_l4_fwd": 2 * B * 64 * f + 2 * B * 32 * f,
+        "k_top": 2 * B * 32 * f + 2 * B * f + 2 * B * 32 * f + slab_w(2 * (D * 32 + D)),
+        "k_bwd_mid": 2 * B * 32 * f * 2 + 2 * B * 64 * f * 2 + slab_w(2 * (32 * 64 + 32)),
+        "k_bwd_first": 2 * B * 64 * f * 2 + B * (nf + nc) * f + slab_w(64 * (nf + nc) + 128),
+        "k_reduce_adam": slab_w(n_params) + 7 * n_params * f,
+    }
+    return fl, by
+
+
+def load_pmc_traffic(name):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary
+    (profiles/*pmc*.json written by tools/pmc_traffic.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        return d.get("kernels", {}).get(name, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(nf, nc, D, B):
+    """Time the CPU oracle on a bounded sample of the same workload."""
+    from oracle import two_tower as O
+    n = 524_288
+    g = torch.Generator().manual_seed(42)
+    data = {
+        "firm_numeric": torch.randn(n, nf, generator=g), "ceo_numeric": torch.randn(n, nc, generator=g),
+        "firm_cat": torch.zeros(n, 0, dtype=torch.int64), "ceo_cat": torch.zeros(n, 0, dtype=torch.int64),
+        "target": torch.randn(n, 1, generator=g),
+    }
+    sd = torch.rand(n, 1, generator=g) * 0.9 + 0.1
+    data["weights"] = 1.0 / (sd * sd + 1e-6)
+    meta = {"n_firm_numeric": nf, "firm_cat_counts": [], "n_ceo_numeric": nc, "ceo_cat_counts": []}
+    torch.manual_seed(42)
+    P = O.init_params_like_reference(meta, D)
+    buf = O.fresh_buffers()
+    opt = O.Adam(P, lr=4e-4)
+    loader = torch.utils.data.DataLoader(O.PairDataset(data), batch_size=B, shuffle=True)
+    t0 = time.perf_counter()
+    pairs, _, buf = O.cpu_train_epoch(P, buf, opt, loader, p=0.1)
+    t_loop = time.perf_counter() - t0
+    batches = [{k: v[i:i + B] for k, v in data.items()} for i in range(0, n, B)]
+    t0 = time.perf_counter()
+    pairs2, _, _ = O.cpu_train_epoch(P, buf, opt, batches, p=0.1)
+    t_comp = time.perf_counter() - t0
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu_model = next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": round(pairs / t_loop, 1), "unit": "pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{n} pairs ({nf}x{nc} feats, D={D}, bs={B}, p=0.1), 1 epoch, oracle reference loop "
+                      f"(per-sample Dataset + DataLoader(shuffle=True)) in {t_loop:.1f}s",
+            "compute_only_pairs_per_s": round(pairs2 / t_comp, 1),
+            "os_cpu_count": os.cpu_count(), "cpu_model": cpu_model}
+
+
+def cosine_roofline(dev, D=128, n=1 << 22, reps=20):
+    from ceo_firm_matching import _native as N
+    L = N.lib()
+    g = torch.Generator(device=dev).manual_seed(7)
+    u = torch.randn(n, D, device=dev, generator=g)
+    v = torch.randn(n, D, device=dev, generator=g)
+    t = torch.randn(n, device=dev, generator=g)
+    w = torch.rand(n, device=dev, generator=g) + 1
+    ls = torch.full((1,), math.log(1 / 0.07), device=dev)
+    score = torch.empty(n, device=dev)
+    du, dv = torch.empty_like(u), torch.empty_like(v)
+    acc = torch.zeros(2, device=dev)
+    st = N.stream_ptr(dev)
+
+    def run():
+        N.check(L.tt_cosine_mse_fwd_bwd(u.data_ptr(), v.data_ptr(), t.data_ptr(), w.data_ptr(), n, D,
+                                        ls.data_ptr(), ctypes.c_float(1.0 / n), score.data_ptr(), du.data_ptr(),
+                                        dv.data_ptr(), acc.data_ptr(), acc.data_ptr() + 4, st), "cosine")
+    for _ in range(3):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    byts = 4 * (4 * D + 3) * n
+    gbs = byts / (ms * 1e-3) / 1e9
+    return {"kernel": "k_cosine<2,true>", "pairs": n, "D": D, "bytes_per_pair": 4 * (4 * D + 3),
+            "avg_us": round(ms * 1e3, 2), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "pairs_per_s": round(n / (ms * 1e-3), 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip roofline / cosine legs")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    from ceo_firm_matching import _native as N
+    from ceo_firm_matching.engine import FusedTrainer
+    from ceo_firm_matching.synthetic import generate_pairs
+
+    n_total, nf, nc, D, B = CONFIGS[args.config]
+    shard = -(-n_total // world)
+    data = generate_pairs(shard, nf, nc, seed=42 + rank, device=dev)
+    meta = {k: data[k] for k in ("n_firm_numeric", "firm_cat_counts", "n_ceo_numeric", "ceo_cat_counts")}
+    cfg = Config()
+    cfg.LATENT_DIM = D
+    cfg.DEVICE = dev
+    torch.manual_seed(42)  # identical init on every rank (DDP broadcast semantics)
+    model = CEOFirmMatcher(meta, cfg).to(dev)
+    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42, process_group=pg)
+    tr.set_data(data)
+    n_batches = shard // B
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    rows = torch.randperm(shard, device=dev, generator=gen)
+
+    use_graph = (world == 1) and not args.no_graph
+    step_fn = lambda: tr.step_cycle(rows, B, n_batches)  # noqa: E731
+    for _ in range(args.warmup):
+        step_fn()
+    torch.cuda.synchronize()
+
+    graph, chunk = None, 1
+    if use_graph:
+        chunk = max(c for c in range(1, 17) if args.steps % c == 0)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step_fn()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(chunk):
+                step_fn()
+        graph.replay()  # one more warm replay
+        torch.cuda.synchronize()
+
+    tr.pop_loss_sum(read=False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if graph is not None:
+        for _ in range(args.steps // chunk):
+            graph.replay()
+    else:
+        for _ in range(args.steps):
+            step_fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = tr.pop_loss_sum() / args.steps
+    pairs = args.steps * B * world
+    value = pairs / elapsed
+
+    result = {
+        "metric": "training pairs/sec (fused fwd+bwd+Adam, CEOFirmMatcher two-tower)",
+        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (N(0,1) features/target, sd~U(0.1,1), w=1/(sd^2+1e-6); random-init weights, "
+                "seed 42), resident in HBM",
+        "config": {"workload": f"{args.config}: {n_total} pairs ({shard}/GPU), {nf}x{nc} feats, LATENT={D}, "
+                               f"bs={B}/GPU, dropout 0.1, Adam lr 4e-4",
+                   "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
+                   "graph": bool(graph is not None), "graph_chunk": chunk},
+        "mean_loss": round(loss, 5),
+    }
+
+    if not args.no_extras:
+        # ---- per-kernel HIP events on the launch stream (separate pass, K steps)
+        st = N.stream_ptr(dev)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(7)] for _ in range(args.steps)]
+        for row in evs:
+            for e in row:
+                e.record()  # materialise the hipEvent
+        torch.cuda.synchronize()
+        a = tr.arena
+        for k in range(args.steps):
+            arr = (ctypes.c_void_p * 7)(*[e.cuda_event for e in evs[k]])
+            batch = tr._batch(rows, 0, B, cycle=n_batches)
+            rc = tr.lib.tt_train_step_ev(tr.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
+                                         batch, tr.hp, tr.seed, tr.state.data_ptr(), tr.ws.data_ptr(),
+                                         tr.ws_bytes, tr.grad.data_ptr(), tr.exp_avg.data_ptr(),
+                                         tr.exp_avg_sq.data_ptr(), int(world == 1), st, arr)
+            N.check(rc, "tt_train_step_ev")
+            if world > 1:
+                tr.allreduce_and_adam()
+        torch.cuda.synchronize()
+        per = {}
+        for i, name in enumerate(KERNELS):
+            per[name] = sum(evs[k][i].elapsed_time(evs[k][i + 1]) for k in range(args.steps)) / args.steps * 1e3
+        fl, by = kernel_work(nf, nc, D, B, a.params.numel(), -(-B // 64))
+        dom = max(per, key=per.get)
+        t_s = per[dom] * 1e-6
+        tf = fl[dom] / t_s / 1e12
+        gbs = by[dom] / t_s / 1e9
+        if tf / PEAK_FP32_TFLOPS >= gbs / PEAK_HBM_GBS:
+            roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tf / PEAK_FP32_TFLOPS, 4), "algorithmic_per_launch": fl[dom]}
+        else:
+            roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_per_launch": by[dom]}
+        roof["kernel"] = dom
+        roof["avg_us"] = round(per[dom], 3)
+        roof["traffic"] = load_pmc_traffic(dom)
+        result["roofline"] = roof
+        result["kernel_us"] = {k: round(v, 3) for k, v in per.items()}
+        result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)
+        if rank == 0:
+            result["cosine_roofline"] = cosine_roofline(dev, D=D)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(nf, nc, D, B)
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

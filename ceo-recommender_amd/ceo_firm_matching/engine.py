@@ -1,0 +1,145 @@
+"""Fused, device-resident training engine for CEOFirmMatcher.
+
+One ``step`` = the reference's training.py:44-57 (zero_grad, forward,
+weighted MSE, backward, Adam.step) as six HIP kernels enqueued by one C-ABI
+call (``tt_train_step``): no per-step host sync, no ``.item()``, no per-sample
+collate.  The dataset lives in HBM; a batch is a slice of a row-index
+permutation that the first kernel gathers from.
+
+Data parallel (one process per GPU, ``torch.distributed`` over RCCL): the
+step stops after the gradient reduction (``apply_adam=0``), the flat fp32
+gradient is all-reduced (AVG, one call per step), and ``tt_adam_apply``
+finishes the step -- DistributedDataParallel semantics with per-rank
+(local) BatchNorm statistics.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from . import _native as N
+from .model import CEOFirmMatcher
+
+DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")
+
+
+class FusedTrainer:
+    def __init__(self, model: CEOFirmMatcher, lr: float = 4e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 max_batch: int = 256, seed: Optional[int] = None, process_group=None):
+        dev = model.logit_scale.device
+        if dev.type != "cuda":
+            raise RuntimeError("FusedTrainer needs the model on a HIP device")
+        self.model = model
+        self.device = dev
+        self.arena = model.bind_arena()
+        self.desc = self.arena.desc
+        self.lib = N.lib()
+        n = self.arena.params.numel()
+        self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        # tt_state: step_done, step_cur (int64), loss_sum (f32), pad
+        self.state = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.hp = N.adam_hp(lr, betas, eps)
+        self.seed = (int(torch.cuda.initial_seed()) if seed is None else int(seed)) & ((1 << 63) - 1)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.max_batch = 0
+        self.ws = None
+        self.ensure_batch(max_batch)
+        self.data: Dict[str, torch.Tensor] = {}
+        self.steps_host = 0
+
+    # ------------------------------------------------------------------ setup
+    def ensure_batch(self, max_batch: int):
+        if max_batch <= self.max_batch:
+            return
+        self.ws_bytes = N.workspace_bytes(self.desc, max_batch)
+        self.ws = torch.zeros(self.ws_bytes // 4, dtype=torch.float32, device=self.device)
+        self.max_batch = max_batch
+
+    def set_data(self, data: Dict[str, torch.Tensor]):
+        """Upload (once) the six dataset arrays of a CEOFirmDataset dict."""
+        out = {}
+        for k in DATA_KEYS:
+            t = data[k]
+            if k in ("firm_cat", "ceo_cat"):
+                t = t.to(device=self.device, dtype=torch.int64)
+                if t.dim() == 1:
+                    t = t.view(-1, 1)
+            elif k in ("target", "weights"):
+                t = t.to(device=self.device, dtype=torch.float32).reshape(-1)
+            else:
+                t = t.to(device=self.device, dtype=torch.float32)
+            out[k] = t.contiguous()
+        g = self.model._geom
+        for t, key in enumerate(("firm_cat", "ceo_cat")):
+            counts = g["cat_counts"][t]
+            c = out[key]
+            if counts and c.numel():
+                hi = torch.tensor(counts, device=self.device)
+                if bool(((c[:, :len(counts)] < 0) | (c[:, :len(counts)] >= hi)).any()):
+                    raise IndexError(f"{key}: category code out of range of its embedding table")
+        self.data = out
+
+    def _batch(self, rows, row0, n_rows, cycle=0, t_base=0):
+        d = self.data
+        return N.make_batch(d["firm_numeric"], d["firm_cat"], d["ceo_numeric"], d["ceo_cat"],
+                            target=d["target"], weight=d["weights"], rows=rows, row0=row0,
+                            n_rows=n_rows, cycle=cycle, t_base=t_base)
+
+    # ------------------------------------------------------------------ steps
+    def _launch(self, batch, n_rows, apply_adam: bool):
+        self.ensure_batch(n_rows)
+        a = self.arena
+        rc = self.lib.tt_train_step(self.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
+                                    batch, self.hp, self.seed, self.state.data_ptr(), self.ws.data_ptr(),
+                                    self.ws_bytes, self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                                    self.exp_avg_sq.data_ptr(), int(apply_adam), N.stream_ptr(self.device))
+        N.check(rc, "tt_train_step", n_rows, 64)
+
+    def step(self, rows: Optional[torch.Tensor], row0: int, n_rows: int):
+        """One optimizer step on dataset rows rows[row0:row0+n_rows]."""
+        batch = self._batch(rows, row0, n_rows)
+        if self.world == 1:
+            self._launch(batch, n_rows, True)
+        else:
+            self._launch(batch, n_rows, False)
+            self.allreduce_and_adam()
+        self.steps_host += 1
+
+    def step_cycle(self, rows: torch.Tensor, batch_size: int, n_batches: int, t_base: int = 0):
+        """Graph-replayable step: batch k = ((t-1-t_base) % n_batches) of
+        ``rows`` taken from the device step counter (no host arguments change
+        between steps)."""
+        batch = self._batch(rows, 0, batch_size, cycle=n_batches, t_base=t_base)
+        if self.world == 1:
+            self._launch(batch, batch_size, True)
+        else:
+            self._launch(batch, batch_size, False)
+            self.allreduce_and_adam()
+        self.steps_host += 1
+
+    def allreduce_and_adam(self):
+        torch.distributed.all_reduce(self.grad, op=torch.distributed.ReduceOp.SUM, group=self.pg)
+        self.grad.mul_(1.0 / self.world)
+        a = self.arena
+        rc = self.lib.tt_adam_apply(a.params.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                                    self.exp_avg_sq.data_ptr(), a.params.numel(), self.hp,
+                                    self.state.data_ptr(), 0, N.stream_ptr(self.device))
+        N.check(rc, "tt_adam_apply")
+
+    # ------------------------------------------------------------------ metrics
+    def loss_sum_tensor(self) -> torch.Tensor:
+        return self.state.view(torch.float32)[4:5]
+
+    def pop_loss_sum(self, read: bool = True) -> Optional[float]:
+        """Sum of batch-mean losses since the last call (reads => host sync)."""
+        t = self.loss_sum_tensor()
+        v = float(t.item()) if read else None
+        t.zero_()
+        return v
+
+    def steps_done(self) -> int:
+        return int(self.state[0].item())

@@ -1,0 +1,258 @@
+"""CEOFirmMatcher -- the two-tower model, MI355X-native.
+
+Drop-in for the reference ``ceo_firm_matching/model.py:14-89``:
+* the same ``nn.Module`` surface: ``CEOFirmMatcher(metadata, config)``,
+  ``forward(f_numeric, f_cat, c_numeric, c_cat) -> [B, 1]``, attributes
+  ``firm_embeddings``/``ceo_embeddings`` (ModuleList), ``firm_tower``/
+  ``ceo_tower`` (indexable ``nn.Sequential``, callable on their own) and
+  ``logit_scale``; identical ``state_dict`` keys; modules are created in the
+  reference order, so ``torch.manual_seed(s)`` gives identical initial weights.
+* On a HIP device the whole forward (embedding gather, both towers, L2
+  normalisation, scaled cosine) and its backward run in the fused kernels of
+  ``libceo_tt.so`` (one autograd node).  Parameters and BatchNorm buffers are
+  re-pointed into one flat fp32 arena (views; ``state_dict``/optimizers keep
+  working) laid out as ``tt_param_offsets`` says.
+* On CPU tensors the module evaluates the same algorithm with ATen ops (there
+  is no HIP kernel to call); this is the reference's own CPU behaviour and is
+  never used for a tensor on a HIP device: a missing extension raises.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native as N
+from .config import Config
+
+TOWERS = ("firm", "ceo")
+
+
+class _Arena:
+    """Flat device storage the kernels address (params / BN buffers / counters)."""
+
+    def __init__(self, desc, params, buffers, nbt, views):
+        self.desc = desc
+        self.params = params
+        self.buffers = buffers
+        self.nbt = nbt
+        self.views = views  # list of (tensor-getter, data_ptr) to validate binding
+
+
+class CEOFirmMatcher(nn.Module):
+    """Two-tower network: firm / CEO encoders + scaled cosine similarity."""
+
+    def __init__(self, metadata: Dict[str, int], config: Config):
+        super().__init__()
+        large = config.EMBEDDING_DIM_LARGE
+        medium = config.EMBEDDING_DIM_MEDIUM
+        p = float(getattr(config, "DROPOUT_P", 0.1))
+        # construction order == reference (model.py:24-65): same RNG draws
+        self.firm_embeddings = nn.ModuleList([nn.Embedding(n, large) for n in metadata['firm_cat_counts']])
+        self.ceo_embeddings = nn.ModuleList([nn.Embedding(n, medium) for n in metadata['ceo_cat_counts']])
+        firm_in = metadata['n_firm_numeric'] + len(metadata['firm_cat_counts']) * large
+        ceo_in = metadata['n_ceo_numeric'] + len(metadata['ceo_cat_counts']) * medium
+        self.firm_tower = self._tower(firm_in, config.LATENT_DIM, p)
+        self.ceo_tower = self._tower(ceo_in, config.LATENT_DIM, p)
+        self.logit_scale = nn.Parameter(torch.ones([]) * np.log(1 / 0.07))
+
+        self._geom = dict(n_num=(int(metadata['n_firm_numeric']), int(metadata['n_ceo_numeric'])),
+                          cat_counts=(list(metadata['firm_cat_counts']), list(metadata['ceo_cat_counts'])),
+                          emb_dim=(large, medium), latent=int(config.LATENT_DIM))
+        self._arena: Optional[_Arena] = None
+        self._stream_step = 0
+        self._aten_warned = False
+
+    @staticmethod
+    def _tower(d_in: int, latent: int, p: float) -> nn.Sequential:
+        return nn.Sequential(
+            nn.Linear(d_in, 64), nn.BatchNorm1d(64), nn.ReLU(), nn.Dropout(p),
+            nn.Linear(64, 32), nn.BatchNorm1d(32), nn.ReLU(), nn.Dropout(p),
+            nn.Linear(32, latent))
+
+    # ------------------------------------------------------------------ helpers
+    def dropout_p(self) -> float:
+        ps = {float(t[i].p) for t in (self.firm_tower, self.ceo_tower) for i in (3, 7)}
+        if len(ps) != 1:
+            raise NotImplementedError("the fused kernels need one dropout probability for all four Dropout layers")
+        return ps.pop()
+
+    def bn_config(self):
+        bns = [t[i] for t in (self.firm_tower, self.ceo_tower) for i in (1, 5)]
+        eps = {float(b.eps) for b in bns}
+        mom = {float(b.momentum) for b in bns}
+        if len(eps) != 1 or len(mom) != 1 or None in mom:
+            raise NotImplementedError("the fused kernels need one BatchNorm eps/momentum")
+        return eps.pop(), mom.pop()
+
+    def tt_desc(self) -> N.TTModelDesc:
+        g = self._geom
+        eps, mom = self.bn_config()
+        return N.make_desc(g["n_num"], g["cat_counts"], g["emb_dim"], g["latent"],
+                           dropout_p=self.dropout_p(), bn_eps=eps, bn_momentum=mom)
+
+    def _named_slots(self, offs):
+        """(name, tensor, float offset) for every parameter in arena order."""
+        out = []
+        for t, tw in enumerate(TOWERS):
+            embs = self.firm_embeddings if t == 0 else self.ceo_embeddings
+            for j, e in enumerate(embs):
+                out.append((f"{tw}_embeddings.{j}.weight", e.weight, offs[t * N.TT_MAX_CAT + j]))
+        for t, tw in enumerate(TOWERS):
+            tower = self.firm_tower if t == 0 else self.ceo_tower
+            for s, nm in enumerate(N.SLOT_NAMES):
+                idx, attr = nm.split(".")
+                out.append((f"{tw}_tower.{nm}", getattr(tower[int(idx)], attr),
+                            offs[2 * N.TT_MAX_CAT + t * N.TT_SLOTS_PER_TOWER + s]))
+        out.append(("logit_scale", self.logit_scale, offs[-1]))
+        return out
+
+    def _bn_modules(self):
+        return [self.firm_tower[1], self.firm_tower[5], self.ceo_tower[1], self.ceo_tower[5]]
+
+    def bind_arena(self) -> _Arena:
+        """Re-point parameters / BN buffers into flat device arenas (idempotent)."""
+        a = self._arena
+        if a is not None and all(get().data_ptr() == p for get, p in a.views):
+            return a
+        desc = self.tt_desc()
+        dev = self.logit_scale.device
+        offs = N.param_offsets(desc)
+        n = N.param_count(desc)
+        params = torch.empty(n, dtype=torch.float32, device=dev)
+        views = []
+        for name, prm, off in self._named_slots(offs):
+            k = prm.numel()
+            v = params[off:off + k].view_as(prm)
+            v.copy_(prm.detach())
+            prm.data = v
+            views.append(((lambda p=prm: p), v.data_ptr()))
+        bns = self._bn_modules()
+        buffers = torch.empty(2 * (2 * 64 + 2 * 32), dtype=torch.float32, device=dev)
+        nbt = torch.empty(4, dtype=torch.int64, device=dev)
+        off = 0
+        for i, bn in enumerate(bns):
+            H = bn.num_features
+            for attr in ("running_mean", "running_var"):
+                v = buffers[off:off + H]
+                v.copy_(getattr(bn, attr).detach().to(torch.float32))
+                setattr(bn, attr, v)
+                views.append(((lambda b=bn, a_=attr: getattr(b, a_)), v.data_ptr()))
+                off += H
+            v = nbt[i]
+            v.copy_(bn.num_batches_tracked.detach())
+            bn.num_batches_tracked = v
+            views.append(((lambda b=bn: b.num_batches_tracked), v.data_ptr()))
+        self._arena = _Arena(desc, params, buffers, nbt, views)
+        return self._arena
+
+    def next_dropout_stream(self):
+        """(seed, step) of the counter-RNG stream for one train-mode forward.
+        The seed follows torch.cuda's (torch.manual_seed) without a sync and
+        without consuming the CPU generator."""
+        self._stream_step += 1
+        return int(torch.cuda.initial_seed()) & ((1 << 63) - 1), self._stream_step
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, f_numeric, f_cat, c_numeric, c_cat):
+        if f_numeric.device.type == "cuda":
+            return _fused_forward(self, f_numeric, f_cat, c_numeric, c_cat)
+        return self._aten_forward(f_numeric, f_cat, c_numeric, c_cat)
+
+    def _aten_forward(self, f_numeric, f_cat, c_numeric, c_cat):
+        """CPU evaluation of model.py:67-89 with ATen ops (no HIP device)."""
+        if not self._aten_warned:
+            warnings.warn("CEOFirmMatcher on CPU tensors: evaluating with ATen ops; the fused HIP "
+                          "kernels run only for tensors on a HIP device", RuntimeWarning, stacklevel=3)
+            self._aten_warned = True
+        f = torch.cat([f_numeric] + [e(f_cat[:, i]) for i, e in enumerate(self.firm_embeddings)], dim=1)
+        c = torch.cat([c_numeric] + [e(c_cat[:, i]) for i, e in enumerate(self.ceo_embeddings)], dim=1)
+        u = self.firm_tower(f)
+        v = self.ceo_tower(c)
+        u = u / u.norm(dim=1, keepdim=True)
+        v = v / v.norm(dim=1, keepdim=True)
+        return (u * v).sum(dim=1, keepdim=True) * self.logit_scale.exp()
+
+
+def _as_f32(x, dev):
+    x = x.to(device=dev, dtype=torch.float32)
+    return x if x.is_contiguous() else x.contiguous()
+
+
+def _as_i64(x, dev):
+    if x is None:
+        return None
+    x = x.to(device=dev, dtype=torch.int64)
+    return x if x.is_contiguous() else x.contiguous()
+
+
+class _FusedTwoTower(torch.autograd.Function):
+    """One autograd node for the whole CEOFirmMatcher forward (HIP kernels)."""
+
+    @staticmethod
+    def forward(ctx, model, f_num, f_cat, c_num, c_cat, *params):
+        arena = model._arena
+        L = N.lib()
+        B = f_num.shape[0]
+        train = bool(model.training)
+        desc = arena.desc
+        ws_bytes = N.workspace_bytes(desc, max(B, 1))
+        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=f_num.device)
+        score = torch.empty(B, dtype=torch.float32, device=f_num.device)
+        seed, step = model.next_dropout_stream() if train else (0, 0)
+        batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
+        rc = L.tt_forward(desc, arena.params.data_ptr(), arena.buffers.data_ptr(), arena.nbt.data_ptr(),
+                          batch, int(train), seed, step, ws.data_ptr(), ws_bytes, score.data_ptr(),
+                          N.stream_ptr(f_num.device))
+        N.check(rc, "tt_forward", B, 64)
+        ctx.model = model
+        ctx.train = train
+        ctx.seed, ctx.step = seed, step
+        ctx.ws, ctx.ws_bytes = ws, ws_bytes
+        ctx.n_params = len(params)
+        ctx.save_for_backward(f_num, f_cat, c_num, c_cat)
+        return score.view(B, 1)
+
+    @staticmethod
+    def backward(ctx, dscore):
+        if not ctx.train:
+            raise NotImplementedError("backward through an eval-mode CEOFirmMatcher forward is not "
+                                      "supported by the fused kernels (call model.train())")
+        f_num, f_cat, c_num, c_cat = ctx.saved_tensors
+        model = ctx.model
+        arena = model._arena
+        B = f_num.shape[0]
+        grad = torch.empty_like(arena.params)
+        ds = dscore.reshape(-1).to(torch.float32).contiguous()
+        batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
+        rc = N.lib().tt_backward(arena.desc, arena.params.data_ptr(), batch, ds.data_ptr(), ctx.seed,
+                                 ctx.step, ctx.ws.data_ptr(), ctx.ws_bytes, grad.data_ptr(),
+                                 N.stream_ptr(f_num.device))
+        N.check(rc, "tt_backward", B, 64)
+        offs = N.param_offsets(arena.desc)
+        grads = [grad[off:off + p.numel()].view_as(p) for _, p, off in model._named_slots(offs)]
+        return (None, None, None, None, None, *grads)
+
+
+def _fused_forward(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
+    dev = f_numeric.device
+    if model.logit_scale.device != dev:
+        raise RuntimeError(f"CEOFirmMatcher parameters are on {model.logit_scale.device}, inputs on {dev}")
+    model.bind_arena()
+    f_num = _as_f32(f_numeric, dev)
+    c_num = _as_f32(c_numeric, dev)
+    f_cat = _as_i64(f_cat, dev)
+    c_cat = _as_i64(c_cat, dev)
+    g = model._geom
+    for t, (num, cat) in enumerate(((f_num, f_cat), (c_num, c_cat))):
+        if num.dim() != 2 or num.shape[1] != g["n_num"][t]:
+            raise RuntimeError(f"tower {TOWERS[t]}: expected [B, {g['n_num'][t]}] numeric input, got {tuple(num.shape)}")
+        if len(g["cat_counts"][t]) and (cat is None or cat.dim() != 2 or cat.shape[1] < len(g["cat_counts"][t])):
+            raise RuntimeError(f"tower {TOWERS[t]}: expected [B, {len(g['cat_counts'][t])}] categorical input")
+    if f_num.shape[0] != c_num.shape[0]:
+        raise RuntimeError("firm and CEO batches differ in size")
+    params = [p for _, p, _ in model._named_slots(N.param_offsets(model._arena.desc))]
+    return _FusedTwoTower.apply(model, f_num, f_cat, c_num, c_cat, *params)

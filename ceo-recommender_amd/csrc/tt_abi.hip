@@ -1,0 +1,540 @@
+// Host side of libceo_tt.so: argument checking, arena / workspace layout and
+// kernel launch sequences behind the C-ABI declared in include/ceo_tt.h.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+
+#include "tt_common.h"
+#include "tt_tower.hip"
+#include "tt_optim.hip"
+#include "tt_cosine.hip"
+
+namespace tt {
+
+constexpr size_t LDS_MAX = 160 * 1024;
+
+// ---------------------------------------------------------------------------
+// layouts
+// ---------------------------------------------------------------------------
+struct Layout {
+  int in_dim[2], kp[2];
+  int64_t emb_off[2][TT_MAX_CAT];
+  int64_t slot[2][TT_SLOTS_PER_TOWER];
+  int64_t ls;
+  int64_t n;          // parameter count
+  int64_t so[2][6];   // slab offsets W0 b0 W4 b4 W8 b8
+  int64_t slab_ld;
+};
+
+static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+static bool desc_ok(const tt_model_desc* d) {
+  if (!d) return false;
+  for (int t = 0; t < 2; ++t) {
+    if (d->n_num[t] < 0 || d->n_cat[t] < 0 || d->n_cat[t] > TT_MAX_CAT) return false;
+    if (d->n_cat[t] > 0 && d->emb_dim[t] <= 0) return false;
+    for (int j = 0; j < d->n_cat[t]; ++j)
+      if (d->cat_counts[t][j] <= 0) return false;
+    if (d->n_num[t] + d->n_cat[t] * d->emb_dim[t] <= 0) return false;
+  }
+  return d->latent > 0 && d->dropout_p >= 0.f && d->dropout_p < 1.f;
+}
+
+static Layout make_layout(const tt_model_desc* d) {
+  Layout L;
+  std::memset(&L, 0, sizeof(L));
+  int64_t off = 0;
+  for (int t = 0; t < 2; ++t)
+    for (int j = 0; j < TT_MAX_CAT; ++j) L.emb_off[t][j] = -1;
+  for (int t = 0; t < 2; ++t)
+    for (int j = 0; j < d->n_cat[t]; ++j) {
+      L.emb_off[t][j] = off;
+      off += (int64_t)d->cat_counts[t][j] * d->emb_dim[t];
+    }
+  const int D = d->latent;
+  for (int t = 0; t < 2; ++t) {
+    const int in = d->n_num[t] + d->n_cat[t] * d->emb_dim[t];
+    L.in_dim[t] = in;
+    L.kp[t] = (int)round_up(in, 16);
+    const int64_t sz[TT_SLOTS_PER_TOWER] = {(int64_t)H0 * in, H0, H0, H0, (int64_t)H1 * H0, H1, H1, H1,
+                                            (int64_t)D * H1, D};
+    for (int s = 0; s < TT_SLOTS_PER_TOWER; ++s) {
+      L.slot[t][s] = off;
+      off += sz[s];
+    }
+    int64_t so = 0;
+    L.so[t][0] = so; so += (int64_t)H0 * in;
+    L.so[t][1] = so; so += H0;
+    L.so[t][2] = so; so += (int64_t)H1 * H0;
+    L.so[t][3] = so; so += H1;
+    L.so[t][4] = so; so += (int64_t)D * H1;
+    L.so[t][5] = so; so += D;
+    L.slab_ld = std::max<int64_t>(L.slab_ld, round_up(so, 64));
+  }
+  L.ls = off;
+  L.n = off + 1;
+  return L;
+}
+
+struct WsLayout {
+  int64_t Z0[2], Z4[2], dY0[2], dY1[2], st0[2], st1[2], sh0[2], sh1[2], fin0[2], fin1[2];
+  int64_t slab[2];
+  int64_t gacc;
+  int64_t total;  // floats
+  int n_tiles;
+};
+
+static WsLayout make_ws(const Layout& L, int64_t max_batch) {
+  WsLayout W;
+  int64_t off = 0;
+  auto take = [&](int64_t n) { const int64_t o = off; off += round_up(n, 64); return o; };
+  W.n_tiles = (int)((max_batch + ROWS - 1) / ROWS);
+  for (int t = 0; t < 2; ++t) {
+    W.Z0[t] = take(max_batch * H0);
+    W.Z4[t] = take(max_batch * H1);
+    W.dY0[t] = take(max_batch * H0);
+    W.dY1[t] = take(max_batch * H1);
+    W.st0[t] = take(2 * H0);
+    W.st1[t] = take(2 * H1);
+    W.sh0[t] = take(H0);
+    W.sh1[t] = take(H1);
+    W.fin0[t] = take(2 * H0);
+    W.fin1[t] = take(2 * H1);
+  }
+  for (int t = 0; t < 2; ++t) W.slab[t] = take((int64_t)W.n_tiles * L.slab_ld);
+  W.gacc = take(L.n);
+  W.total = off;
+  return W;
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+static std::once_flag g_attr_once;
+static void set_lds_attrs() {
+  std::call_once(g_attr_once, [] {
+    const int mx = (int)LDS_MAX;
+    (void)hipFuncSetAttribute((const void*)k_l0_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_l4_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_top<4>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_top<8>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_bwd_mid, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_bwd_first, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+  });
+}
+
+struct Plan {
+  size_t lds_l0, lds_l4, lds_top, lds_mid, lds_first;
+  int ndt;
+};
+
+static int make_plan(const tt_model_desc* d, const Layout& L, Plan* P) {
+  if (d->latent > 128) return TT_ERR_UNSUPPORTED;
+  P->ndt = d->latent <= 64 ? 4 : 8;
+  const int kpm = std::max(L.kp[0], L.kp[1]);
+  if (kpm > MAX_KP) return TT_ERR_UNSUPPORTED;
+  const bool emb = d->n_cat[0] > 0 || d->n_cat[1] > 0;
+  P->lds_l0 = lds_l0_fwd(kpm);
+  P->lds_l4 = lds_l4_fwd();
+  P->lds_top = lds_top(P->ndt);
+  P->lds_mid = lds_bwd_mid();
+  P->lds_first = lds_bwd_first(kpm, emb);
+  for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first})
+    if (s > LDS_MAX) return TT_ERR_UNSUPPORTED;
+  return TT_OK;
+}
+
+static bool batch_ok(const tt_model_desc* d, const tt_batch* b) {
+  if (!b || b->n_rows < 0) return false;
+  for (int t = 0; t < 2; ++t) {
+    if (d->n_num[t] > 0 && (!b->num[t] || b->num_ld[t] < d->n_num[t])) return false;
+    if (d->n_cat[t] > 0 && (!b->cat[t] || b->cat_ld[t] < d->n_cat[t])) return false;
+  }
+  return true;
+}
+
+static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, const WsLayout& W, const float* params,
+                      float* buffers, int64_t* nbt, const tt_batch* b, float* ws) {
+  std::memset(&a, 0, sizeof(a));
+  for (int t = 0; t < 2; ++t) {
+    TowerDev& T = a.tw[t];
+    T.num = b->num[t];
+    T.num_ld = b->num_ld[t];
+    T.cat = b->cat[t];
+    T.cat_ld = b->cat_ld[t];
+    T.n_num = d->n_num[t];
+    T.n_cat = d->n_cat[t];
+    T.emb_dim = d->n_cat[t] > 0 ? d->emb_dim[t] : 1;
+    T.in_dim = L.in_dim[t];
+    T.kp = L.kp[t];
+    float* gacc = ws + W.gacc;
+    for (int j = 0; j < d->n_cat[t]; ++j) {
+      T.emb[j] = params + L.emb_off[t][j];
+      T.gemb[j] = gacc + L.emb_off[t][j];
+      T.emb_rows[j] = d->cat_counts[t][j];
+    }
+    const int64_t* s = L.slot[t];
+    T.W0 = params + s[TT_SLOT_W0];
+    T.b0 = params + s[TT_SLOT_B0];
+    T.g0 = params + s[TT_SLOT_G0];
+    T.be0 = params + s[TT_SLOT_BE0];
+    T.W4 = params + s[TT_SLOT_W4];
+    T.b4 = params + s[TT_SLOT_B4];
+    T.g1 = params + s[TT_SLOT_G1];
+    T.be1 = params + s[TT_SLOT_BE1];
+    T.W8 = params + s[TT_SLOT_W8];
+    T.b8 = params + s[TT_SLOT_B8];
+    if (buffers) {  // NULL for backward (running stats untouched)
+      float* bt = buffers + t * (2 * H0 + 2 * H1);
+      T.rm0 = bt;
+      T.rv0 = bt + H0;
+      T.rm1 = bt + 2 * H0;
+      T.rv1 = bt + 2 * H0 + H1;
+    }
+    if (nbt) {
+      T.nbt0 = nbt + 2 * t;
+      T.nbt1 = nbt + 2 * t + 1;
+    }
+    T.gg0 = gacc + s[TT_SLOT_G0];
+    T.gbe0 = gacc + s[TT_SLOT_BE0];
+    T.gg1 = gacc + s[TT_SLOT_G1];
+    T.gbe1 = gacc + s[TT_SLOT_BE1];
+    T.Z0 = ws + W.Z0[t];
+    T.Z4 = ws + W.Z4[t];
+    T.dY0 = ws + W.dY0[t];
+    T.dY1 = ws + W.dY1[t];
+    T.st0 = ws + W.st0[t];
+    T.st1 = ws + W.st1[t];
+    T.shift0 = ws + W.sh0[t];
+    T.shift1 = ws + W.sh1[t];
+    T.fin0 = ws + W.fin0[t];
+    T.fin1 = ws + W.fin1[t];
+    T.slab = ws + W.slab[t];
+    T.so_W0 = L.so[t][0];
+    T.so_b0 = L.so[t][1];
+    T.so_W4 = L.so[t][2];
+    T.so_b4 = L.so[t][3];
+    T.so_W8 = L.so[t][4];
+    T.so_b8 = L.so[t][5];
+  }
+  a.target = b->target;
+  a.weight = b->weight;
+  a.rows = b->rows;
+  a.row0 = b->row0;
+  a.B = b->n_rows;
+  a.cycle = b->cycle;
+  a.t_base = b->t_base;
+  a.eps = d->bn_eps;
+  a.momentum = d->bn_momentum;
+  const double thr = (double)d->dropout_p * 16777216.0;
+  a.drop_thr = (uint32_t)thr;
+  a.drop_scale = a.drop_thr > 0 ? 1.0f / (1.0f - d->dropout_p) : 1.0f;
+  a.D = d->latent;
+  a.n_tiles = (int)((b->n_rows + ROWS - 1) / ROWS);
+  a.slab_ld = (int)L.slab_ld;
+  a.logit_scale = params + L.ls;
+  a.g_ls = ws + W.gacc + L.ls;
+}
+
+static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout& W, float* ws, int n_slabs,
+                        float* grad) {
+  RedArgs r;
+  std::memset(&r, 0, sizeof(r));
+  int k = 0;
+  auto add = [&](int64_t off, int64_t len, int kind, int tower, int64_t so) {
+    if (len <= 0) return;
+    r.seg[k].off = off;
+    r.seg[k].len = len;
+    r.seg[k].kind = kind;
+    r.seg[k].tower = tower;
+    r.seg[k].slab_off = so;
+    ++k;
+  };
+  int64_t emb_total = L.slot[0][TT_SLOT_W0];
+  add(0, emb_total, 1, 0, 0);
+  for (int t = 0; t < 2; ++t) {
+    const int64_t* s = L.slot[t];
+    add(s[TT_SLOT_W0], s[TT_SLOT_G0] - s[TT_SLOT_W0], 0, t, L.so[t][0]);
+    add(s[TT_SLOT_G0], s[TT_SLOT_W4] - s[TT_SLOT_G0], 1, t, 0);
+    add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2]);
+    add(s[TT_SLOT_G1], s[TT_SLOT_W8] - s[TT_SLOT_G1], 1, t, 0);
+    add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], 0, t, L.so[t][4]);
+  }
+  add(L.ls, 1, 1, 0, 0);
+  r.n_seg = k;
+  r.n_slabs = n_slabs;
+  r.n = L.n;
+  r.slab[0] = ws + W.slab[0];
+  r.slab[1] = ws + W.slab[1];
+  r.slab_ld = L.slab_ld;
+  r.gacc = ws + W.gacc;
+  r.grad = grad;
+  return r;
+}
+
+static int launch_check() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? TT_OK : (int)e;
+}
+
+struct Ctx {
+  Layout L;
+  WsLayout W;
+  Plan P;
+};
+
+static int prepare(const tt_model_desc* d, const tt_batch* b, int64_t ws_bytes, Ctx* c) {
+  if (!desc_ok(d) || !batch_ok(d, b)) return TT_ERR_ARG;
+  c->L = make_layout(d);
+  int rc = make_plan(d, c->L, &c->P);
+  if (rc) return rc;
+  c->W = make_ws(c->L, std::max<int64_t>(b->n_rows, 1));
+  if ((int64_t)(c->W.total * sizeof(float)) > ws_bytes) return TT_ERR_WORKSPACE;
+  set_lds_attrs();
+  return TT_OK;
+}
+
+static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s) {
+  const dim3 grid(a.n_tiles, grid_y);
+  if (P.ndt == 4)
+    hipLaunchKernelGGL(k_top<4>, grid, dim3(THREADS), P.lds_top, s, a);
+  else
+    hipLaunchKernelGGL(k_top<8>, grid, dim3(THREADS), P.lds_top, s, a);
+}
+
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" {
+
+int32_t tt_abi_version(void) { return TT_ABI_VERSION; }
+
+int64_t tt_param_count(const tt_model_desc* d) {
+  if (!desc_ok(d)) return TT_ERR_ARG;
+  return make_layout(d).n;
+}
+
+int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out) {
+  if (!desc_ok(d) || !out) return TT_ERR_ARG;
+  const Layout L = make_layout(d);
+  for (int t = 0; t < 2; ++t)
+    for (int j = 0; j < TT_MAX_CAT; ++j) out[t * TT_MAX_CAT + j] = L.emb_off[t][j];
+  for (int t = 0; t < 2; ++t)
+    for (int s = 0; s < TT_SLOTS_PER_TOWER; ++s) out[2 * TT_MAX_CAT + t * TT_SLOTS_PER_TOWER + s] = L.slot[t][s];
+  out[2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER] = L.ls;
+  return TT_OK;
+}
+
+int64_t tt_buffer_count(const tt_model_desc* d) {
+  if (!desc_ok(d)) return TT_ERR_ARG;
+  return 2 * (2 * H0 + 2 * H1);
+}
+
+int64_t tt_workspace_bytes(const tt_model_desc* d, int64_t max_batch) {
+  if (!desc_ok(d) || max_batch < 1) return TT_ERR_ARG;
+  const Layout L = make_layout(d);
+  return make_ws(L, max_batch).total * (int64_t)sizeof(float);
+}
+
+int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, int64_t* nbt, const tt_batch* b,
+                   int32_t train, uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* score,
+                   tt_stream_t stream) {
+  if (!params || !buffers || !nbt || !ws || !score) return TT_ERR_ARG;
+  Ctx c;
+  int rc = prepare(d, b, ws_bytes, &c);
+  if (rc) return rc;
+  if (train && b->n_rows < 2) return TT_ERR_BATCH_TOO_SMALL;
+  if (b->n_rows == 0) return TT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  StepArgs a;
+  fill_args(a, d, c.L, c.W, params, buffers, nbt, b, w);
+  a.train = train ? 1 : 0;
+  a.update_stats = a.train;
+  a.seed = seed;
+  a.step_host = step;
+  a.mode = TOP_FWD;
+  a.score = score;
+  if (train) {
+    for (int t = 0; t < 2; ++t) {
+      (void)hipMemsetAsync(w + c.W.st0[t], 0, sizeof(float) * 2 * H0, s);
+      (void)hipMemsetAsync(w + c.W.st1[t], 0, sizeof(float) * 2 * H1, s);
+    }
+  }
+  const dim3 grid(a.n_tiles, 2);
+  hipLaunchKernelGGL(k_l0_fwd, grid, dim3(THREADS), c.P.lds_l0, s, a);
+  hipLaunchKernelGGL(k_l4_fwd, grid, dim3(THREADS), c.P.lds_l4, s, a);
+  launch_top(a, c.P, 1, s);
+  return launch_check();
+}
+
+int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch* b, const float* dscore,
+                    uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream) {
+  if (!params || !dscore || !ws || !grad) return TT_ERR_ARG;
+  Ctx c;
+  int rc = prepare(d, b, ws_bytes, &c);
+  if (rc) return rc;
+  if (b->n_rows < 2) return TT_ERR_BATCH_TOO_SMALL;
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  // running-stat buffers are not touched by backward; pass a dummy-safe pointer
+  StepArgs a;
+  fill_args(a, d, c.L, c.W, params, nullptr, nullptr, b, w);
+  a.train = 1;
+  a.update_stats = 0;
+  a.seed = seed;
+  a.step_host = step;
+  a.mode = TOP_BWD_GIVEN;
+  a.dscore = dscore;
+  (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
+  const dim3 grid(a.n_tiles, 2);
+  launch_top(a, c.P, 2, s);
+  hipLaunchKernelGGL(k_bwd_mid, grid, dim3(THREADS), c.P.lds_mid, s, a);
+  hipLaunchKernelGGL(k_bwd_first, grid, dim3(THREADS), c.P.lds_first, s, a);
+  RedArgs r = make_red(d, c.L, c.W, w, a.n_tiles, grad);
+  const int nb = (int)((c.L.n + RED_E - 1) / RED_E);
+  hipLaunchKernelGGL(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, r);
+  return launch_check();
+}
+
+static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
+                               const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws,
+                               int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq, int32_t apply_adam,
+                               tt_stream_t stream, void* const* events) {
+  if (!params || !buffers || !nbt || !state || !ws || !grad) return TT_ERR_ARG;
+  if (apply_adam && (!hp || !exp_avg || !exp_avg_sq)) return TT_ERR_ARG;
+  if (b && b->cycle > 0 && b->n_rows < 1) return TT_ERR_ARG;
+  Ctx c;
+  int rc = prepare(d, b, ws_bytes, &c);
+  if (rc) return rc;
+  if (b->n_rows < 2) return TT_ERR_BATCH_TOO_SMALL;
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  StepArgs a;
+  fill_args(a, d, c.L, c.W, params, buffers, nbt, b, w);
+  a.train = 1;
+  a.update_stats = 1;
+  a.seed = seed;
+  a.state = state;
+  a.mode = TOP_TRAIN;
+  a.loss_sum = &state->loss_sum;
+  const dim3 grid(a.n_tiles, 2);
+  auto ev = [&](int k) {
+    if (events && events[k]) (void)hipEventRecord((hipEvent_t)events[k], s);
+  };
+  ev(0);
+  hipLaunchKernelGGL(k_l0_fwd, grid, dim3(THREADS), c.P.lds_l0, s, a);
+  ev(1);
+  hipLaunchKernelGGL(k_l4_fwd, grid, dim3(THREADS), c.P.lds_l4, s, a);
+  ev(2);
+  launch_top(a, c.P, 2, s);
+  ev(3);
+  hipLaunchKernelGGL(k_bwd_mid, grid, dim3(THREADS), c.P.lds_mid, s, a);
+  ev(4);
+  hipLaunchKernelGGL(k_bwd_first, grid, dim3(THREADS), c.P.lds_first, s, a);
+  ev(5);
+  RedArgs r = make_red(d, c.L, c.W, w, a.n_tiles, grad);
+  for (int t = 0; t < 2; ++t) {
+    r.zero_buf[2 * t] = w + c.W.st0[t];
+    r.zero_len[2 * t] = 2 * H0;
+    r.zero_buf[2 * t + 1] = w + c.W.st1[t];
+    r.zero_len[2 * t + 1] = 2 * H1;
+  }
+  if (apply_adam) {
+    r.apply_adam = 1;
+    r.p = params;
+    r.m = exp_avg;
+    r.v = exp_avg_sq;
+    r.lr = hp->lr;
+    r.b1 = hp->beta1;
+    r.b2 = hp->beta2;
+    r.eps = hp->eps;
+    r.state = state;
+  }
+  const int nb = (int)((c.L.n + RED_E - 1) / RED_E);
+  hipLaunchKernelGGL(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, r);
+  ev(6);
+  return launch_check();
+}
+
+int32_t tt_train_step(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt, const tt_batch* b,
+                      const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws, int64_t ws_bytes, float* grad,
+                      float* exp_avg, float* exp_avg_sq, int32_t apply_adam, tt_stream_t stream) {
+  return train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg, exp_avg_sq,
+                         apply_adam, stream, nullptr);
+}
+
+int32_t tt_train_step_ev(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt, const tt_batch* b,
+                         const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws, int64_t ws_bytes,
+                         float* grad, float* exp_avg, float* exp_avg_sq, int32_t apply_adam, tt_stream_t stream,
+                         void* const* events) {
+  return train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg, exp_avg_sq,
+                         apply_adam, stream, events);
+}
+
+int32_t tt_adam_apply(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                      const tt_adam_hp* hp, tt_state* state, int64_t step_host, tt_stream_t stream) {
+  if (!params || !grad || !exp_avg || !exp_avg_sq || !hp || n < 0) return TT_ERR_ARG;
+  if (!state && step_host < 1) return TT_ERR_ARG;
+  if (n == 0) return TT_OK;
+  const int nb = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_adam, dim3(nb), dim3(256), 0, (hipStream_t)stream, params, grad, exp_avg, exp_avg_sq, n,
+                     hp->lr, hp->beta1, hp->beta2, hp->eps, state, step_host);
+  return launch_check();
+}
+
+static int cosine_launch(const float* u, const float* v, const float* tg, const float* wt, int64_t B, int32_t D,
+                         const float* ls, float inv_batch, float* score, float* du, float* dv, float* loss,
+                         float* dls, bool bwd, hipStream_t s) {
+  if (!u || !v || !ls || !score || B < 0 || D <= 0) return TT_ERR_ARG;
+  if (bwd && (!tg || !wt || !du || !dv || !loss || !dls)) return TT_ERR_ARG;
+  if (B == 0) return TT_OK;
+  const int64_t rows_per_block = 256 / 16;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((B + rows_per_block - 1) / rows_per_block, 4096));
+  const dim3 g(nb), t(256);
+  const bool vec = (D % 4 == 0) && ((uintptr_t)u % 16 == 0) && ((uintptr_t)v % 16 == 0) &&
+                   (!bwd || ((uintptr_t)du % 16 == 0 && (uintptr_t)dv % 16 == 0));
+  const int n4 = D / 4;
+#define TT_COS(NV)                                                                                             \
+  do {                                                                                                         \
+    if (bwd)                                                                                                   \
+      hipLaunchKernelGGL((k_cosine<NV, true>), g, t, 0, s, u, v, tg, wt, B, D, ls, inv_batch, score, du, dv,  \
+                         loss, dls);                                                                           \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_cosine<NV, false>), g, t, 0, s, u, v, tg, wt, B, D, ls, inv_batch, score, du, dv, \
+                         loss, dls);                                                                           \
+  } while (0)
+  if (vec && n4 <= 16)
+    TT_COS(1);
+  else if (vec && n4 <= 32)
+    TT_COS(2);
+  else if (vec && n4 <= 64)
+    TT_COS(4);
+  else if (vec && n4 <= 128)
+    TT_COS(8);
+  else if (bwd)
+    hipLaunchKernelGGL((k_cosine_scalar<true>), g, t, 0, s, u, v, tg, wt, B, D, ls, inv_batch, score, du, dv, loss,
+                       dls);
+  else
+    hipLaunchKernelGGL((k_cosine_scalar<false>), g, t, 0, s, u, v, tg, wt, B, D, ls, inv_batch, score, du, dv, loss,
+                       dls);
+#undef TT_COS
+  return launch_check();
+}
+
+int32_t tt_cosine_forward(const float* u, const float* v, int64_t B, int32_t D, const float* logit_scale,
+                          float* score, tt_stream_t stream) {
+  return cosine_launch(u, v, nullptr, nullptr, B, D, logit_scale, 0.f, score, nullptr, nullptr, nullptr, nullptr,
+                       false, (hipStream_t)stream);
+}
+
+int32_t tt_cosine_mse_fwd_bwd(const float* u, const float* v, const float* target, const float* weight, int64_t B,
+                              int32_t D, const float* logit_scale, float inv_batch, float* score, float* du,
+                              float* dv, float* loss_sum, float* dls_sum, tt_stream_t stream) {
+  return cosine_launch(u, v, target, weight, B, D, logit_scale, inv_batch, score, du, dv, loss_sum, dls_sum, true,
+                       (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,213 @@
+// Shared device helpers for the two-tower (CEOFirmMatcher) training kernels.
+//
+// gfx950 / CDNA4 only: wave64, v_mfma_f32_16x16x4_f32 (exact fp32 MFMA),
+// ds_add_f32 LDS atomics, global_atomic_add_f32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ceo_tt.h"
+
+namespace tt {
+
+constexpr int WAVE = 64;
+constexpr int H0 = 64;    // model.py:38  Linear(in, 64)
+constexpr int H1 = 32;    // model.py:42  Linear(64, 32)
+constexpr int ROWS = 64;  // rows of the batch per row tile (one 16-row strip per wave)
+constexpr int WAVES = ROWS / 16;
+constexpr int THREADS = WAVES * WAVE;
+constexpr int MAX_KP = 256;  // padded tower input width supported by the fused kernels
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// ---------------------------------------------------------------------------
+// v_mfma_f32_16x16x4_f32, fp32 in / fp32 acc (bitwise an fmaf chain).
+//   lane l supplies A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15];
+//   C/D: lane l holds C[row = 4*(l>>4) + reg][col = l&15].
+// Our K order: MFMA step s of a 16-wide K chunk k0 uses k = k0 + 4*(l>>4) + s,
+// so every lane reads 4 consecutive k with ONE ds_read_b128 per operand.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void mfma_k16(const float4& a, const float4& b, f32x4& c) {
+  c = mfma4(a.x, b.x, c);
+  c = mfma4(a.y, b.y, c);
+  c = mfma4(a.z, b.z, c);
+  c = mfma4(a.w, b.w, c);
+}
+
+// Row-strip NT GEMM from LDS:  C[16 x 16*NT] = A[16 x K] * B[16*NT x K]^T
+//   A: this wave's 16-row strip, row-major, stride lda (floats)
+//   B: row-major [n][k], stride ldb;  K a multiple of 16 (zero padded)
+template <int NT>
+__device__ __forceinline__ void strip_gemm_nt(const float* A, int lda, const float* B, int ldb,
+                                              int K, f32x4 (&acc)[NT]) {
+  const int l = lane_id(), r = l & 15, g = l >> 4;
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    const float4 a = *reinterpret_cast<const float4*>(A + r * lda + k0 + 4 * g);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float4 b = *reinterpret_cast<const float4*>(B + (16 * j + r) * ldb + k0 + 4 * g);
+      mfma_k16(a, b, acc[j]);
+    }
+  }
+}
+
+// Rows-contracted product from C-layout registers (no LDS):
+//   acc[16 x 16] += P^T Q  over this wave's 16 rows, where P, Q are 16x16 tiles
+//   held in C layout (lane (r,g) holds rows 4g..4g+3 of column r).
+__device__ __forceinline__ void cl_gemm_tn(const f32x4& P, const f32x4& Q, f32x4& acc) {
+  acc = mfma4(P[0], Q[0], acc);
+  acc = mfma4(P[1], Q[1], acc);
+  acc = mfma4(P[2], Q[2], acc);
+  acc = mfma4(P[3], Q[3], acc);
+}
+
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// sum over the 4 lane groups (g = l>>4) that share a column r
+__device__ __forceinline__ float col_reduce(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+// sum over the 16 lanes (r) that share a row group g
+__device__ __forceinline__ float row_reduce16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Counter-based dropout RNG (restated in oracle/two_tower.py dropout_keep_mask)
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t dropout_key(uint64_t seed, uint64_t step, int tower, int layer) {
+  return mix64(seed * 0x9E3779B97F4A7C15ull + step * 0xD1B54A32D192ED03ull +
+               (uint64_t)(tower * 2 + layer + 1) * 0x8CB92BA72F3D8DD7ull);
+}
+__device__ __forceinline__ bool dropout_keep(uint64_t key, uint64_t ctr, uint32_t thr) {
+  const uint64_t h = mix64(key + ctr * 0x9E3779B97F4A7C15ull);
+  return (uint32_t)(h >> 40) >= thr;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel argument block (passed by value; lives in the kernarg segment).
+// ---------------------------------------------------------------------------
+struct TowerDev {
+  const float* num;  int64_t num_ld;      // numeric features [N, num_ld]
+  const int64_t* cat; int64_t cat_ld;     // categorical codes [N, cat_ld]
+  int n_num, n_cat, emb_dim, in_dim, kp;  // kp = in_dim rounded up to 16
+  const float* emb[TT_MAX_CAT];           // embedding tables (param arena)
+  int emb_rows[TT_MAX_CAT];               // rows per table (codes are clamped into range)
+  float* gemb[TT_MAX_CAT];                // their gradient accumulators (gacc arena)
+  const float *W0, *b0, *g0, *be0, *W4, *b4, *g1, *be1, *W8, *b8;
+  float *rm0, *rv0, *rm1, *rv1;           // BN running stats
+  int64_t *nbt0, *nbt1;                   // num_batches_tracked
+  float *gg0, *gbe0, *gg1, *gbe1;         // BN affine grad accumulators (gacc arena)
+  // workspace
+  float *Z0, *Z4, *dY0, *dY1;             // [B,64] [B,32] [B,64] [B,32]
+  float *st0, *st1;                       // shifted moment sums S1|S2 [2*64], [2*32]
+  float *shift0, *shift1;                 // shifts used for S1/S2 [64], [32]
+  float *fin0, *fin1;                     // finalized mean|invstd [2*64], [2*32]
+  float* slab;                            // [n_slabs][slab_ld] partial dW/db sums
+  int64_t so_W0, so_b0, so_W4, so_b4, so_W8, so_b8;  // offsets inside one slab
+};
+
+enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2 };
+
+struct StepArgs {
+  TowerDev tw[2];
+  // batch
+  const float* target; const float* weight;  // [N] each
+  const int64_t* rows;   // row index list (nullable: identity)
+  int64_t row0;          // host-mode offset into rows / dataset
+  int64_t B;             // rows in this batch
+  int64_t cycle;         // >0: device-counter mode, batch k starts at ((t-1-t_base)%cycle)*B
+  int64_t t_base;
+  tt_state* state;       // device counters (nullable: host mode)
+  int64_t step_host;     // host-mode step number (dropout stream / Adam t)
+  uint64_t seed;
+  uint32_t drop_thr;     // keep iff 24-bit hash >= drop_thr  (0: no dropout)
+  float drop_scale;      // 1/(1-p) as fp32
+  float eps, momentum;
+  int train;
+  int update_stats;      // fold batch stats into running stats (forward of a train step)
+  int D, n_tiles, slab_ld;
+  int mode;              // TopMode for the top kernel
+  const float* logit_scale;
+  float* g_ls;           // gacc slot of logit_scale
+  float* score;          // [B] output scores (nullable)
+  const float* dscore;   // [B] upstream grad (TOP_BWD_GIVEN)
+  float* loss_sum;       // [1] += sum w (s-t)^2 / B   (TOP_TRAIN)
+};
+
+__device__ __forceinline__ int64_t step_for_first_kernel(const StepArgs& a) {
+  return a.state ? a.state->step_done + 1 : a.step_host;
+}
+__device__ __forceinline__ int64_t step_current(const StepArgs& a) {
+  return a.state ? a.state->step_cur : a.step_host;
+}
+__device__ __forceinline__ int64_t batch_row0(const StepArgs& a, int64_t t) {
+  if (a.cycle > 0) return ((t - 1 - a.t_base) % a.cycle) * a.B;
+  return a.row0;
+}
+// dataset row of batch row i
+__device__ __forceinline__ int64_t data_row(const StepArgs& a, int64_t base, int64_t i) {
+  return a.rows ? a.rows[base + i] : base + i;
+}
+
+// X[row][col] of a tower input (numeric ++ embeddings), col < kp (zero pad)
+__device__ __forceinline__ float tower_x(const TowerDev& T, int64_t drow, int col) {
+  if (col < T.n_num) return T.num[drow * T.num_ld + col];
+  if (col >= T.in_dim) return 0.f;
+  const int c = col - T.n_num;
+  const int j = c / T.emb_dim, e = c - j * T.emb_dim;
+  int64_t code = T.cat[drow * T.cat_ld + j];
+  code = code < 0 ? 0 : (code >= T.emb_rows[j] ? T.emb_rows[j] - 1 : code);
+  return T.emb[j][code * T.emb_dim + e];
+}
+
+// ---------------------------------------------------------------------------
+// gradient reduction / Adam arguments (tt_optim.hip)
+// ---------------------------------------------------------------------------
+constexpr int MAX_SEG = 48;
+constexpr int RED_E = 32;   // elements per block
+constexpr int RED_G = 8;    // slab groups per element
+
+struct Seg {
+  int64_t off, len;      // range in the parameter arena
+  int64_t slab_off;      // offset of the range inside a tower slab (kind 0)
+  int32_t kind, tower;   // kind 0: slab partials, 1: atomic accumulator (gacc)
+};
+
+struct RedArgs {
+  Seg seg[MAX_SEG];
+  int32_t n_seg;
+  int32_t n_slabs;
+  int64_t n;
+  const float* slab[2];
+  int64_t slab_ld;
+  float* gacc;
+  float* grad;
+  float* zero_buf[4];
+  int32_t zero_len[4];
+  int32_t apply_adam;
+  float* p; float* m; float* v;
+  float lr, b1, b2, eps;
+  tt_state* state;
+  int64_t step_host;
+};
+
+}  // namespace tt

@@ -1,0 +1,100 @@
+// Gradient reduction + Adam over the flat parameter arena (gfx950).
+//
+// k_reduce_adam : for every parameter element, sum its per-row-tile partial
+//   slabs (dW/db written by the tower kernels) in a fixed order -- or take the
+//   atomically accumulated value (BN affine, embeddings, logit_scale) -- write
+//   the full gradient, zero the accumulators for the next step, and optionally
+//   apply Adam in the same pass (single-GPU training: one launch for K10+K11).
+// k_adam : Adam alone (data-parallel: after the RCCL all-reduce of `grad`).
+//
+// Adam arithmetic follows torch 2.10 _single_tensor_adam (optim.Adam.step,
+// training.py:55):  m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+//   denom = sqrt(v) / sqrt(bc2) + eps;  p.addcdiv_(m, denom, -lr/bc1)
+// with bias corrections in double precision, element math in fp32.
+#include "tt_common.h"
+
+namespace tt {
+
+struct AdamCoef {
+  float w1, c2, b2, step_size, bc2s, eps;
+};
+
+__device__ __forceinline__ AdamCoef adam_coef(float lr, float b1, float b2, float eps, int64_t t) {
+  const double bc1 = 1.0 - pow((double)b1, (double)t);
+  const double bc2 = 1.0 - pow((double)b2, (double)t);
+  AdamCoef c;
+  c.w1 = (float)(1.0 - (double)b1);
+  c.c2 = (float)(1.0 - (double)b2);
+  c.b2 = b2;
+  c.step_size = (float)((double)lr / bc1);
+  c.bc2s = (float)sqrt(bc2);
+  c.eps = eps;
+  return c;
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamCoef& c) {
+  m = m + c.w1 * (g - m);           // lerp, weight < 0.5 branch
+  v = v * c.b2 + (c.c2 * g) * g;    // mul_ + addcmul_
+  const float denom = sqrtf(v) / c.bc2s + c.eps;
+  p = p + (-c.step_size) * (m / denom);
+}
+
+__global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
+  __shared__ float part[RED_G][RED_E];
+  const int el = threadIdx.x & (RED_E - 1), pg = threadIdx.x / RED_E;
+  const int64_t e = (int64_t)blockIdx.x * RED_E + el;
+  int si = -1;
+  if (e < a.n)
+    for (int k = 0; k < a.n_seg; ++k)
+      if (e >= a.seg[k].off && e < a.seg[k].off + a.seg[k].len) { si = k; break; }
+  float acc = 0.f;
+  if (si >= 0) {
+    const Seg& S = a.seg[si];
+    if (S.kind == 0) {
+      const float* base = a.slab[S.tower] + S.slab_off + (e - S.off);
+      for (int p = pg; p < a.n_slabs; p += RED_G) acc += base[(int64_t)p * a.slab_ld];
+    } else if (pg == 0) {
+      acc = a.gacc[e];
+    }
+  }
+  part[pg][el] = acc;
+  // zero the BN moment sums consumed by this step (one block)
+  if (blockIdx.x == 0)
+    for (int b = 0; b < 4; ++b)
+      for (int i = threadIdx.x; i < a.zero_len[b]; i += blockDim.x) a.zero_buf[b][i] = 0.f;
+  __syncthreads();
+  if (pg != 0 || si < 0) return;
+  float gsum = 0.f;
+#pragma unroll
+  for (int k = 0; k < RED_G; ++k) gsum += part[k][el];
+  a.grad[e] = gsum;
+  if (a.seg[si].kind == 1) a.gacc[e] = 0.f;
+  if (a.apply_adam) {
+    const int64_t t = a.state ? a.state->step_cur : a.step_host;
+    const AdamCoef c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+    float p = a.p[e], m = a.m[e], v = a.v[e];
+    adam_elem(p, m, v, gsum, c);
+    a.p[e] = p;
+    a.m[e] = m;
+    a.v[e] = v;
+    if (a.state && blockIdx.x == 0 && el == 0) a.state->step_done = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ P, const float* __restrict__ G,
+                                              float* __restrict__ M, float* __restrict__ V, int64_t n,
+                                              float lr, float b1, float b2, float eps, tt_state* state,
+                                              int64_t step_host) {
+  const int64_t t = state ? state->step_cur : step_host;
+  const AdamCoef c = adam_coef(lr, b1, b2, eps, t);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float p = P[e], m = M[e], v = V[e];
+    adam_elem(p, m, v, G[e], c);
+    P[e] = p;
+    M[e] = m;
+    V[e] = v;
+  }
+  if (state && blockIdx.x == 0 && threadIdx.x == 0) state->step_done = t;
+}
+
+}  // namespace tt

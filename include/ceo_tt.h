@@ -1,0 +1,171 @@
+/*
+ * ceo_tt.h -- C-ABI of the MI355X-native CEOFirmMatcher two-tower training
+ * path (libceo_tt.so, HIP / gfx950).
+ *
+ * The reference (SMaric93/CEO-Recommender) is pure Python: its hot path is
+ * ATen ops issued by CEOFirmMatcher.forward, loss.backward() and
+ * optim.Adam.step().  It has no FFI of its own, so every entry point below
+ * names the reference code it replaces (file:line under the reference's
+ * ceo_firm_matching/ package).  The Python mirror that binds them with ctypes
+ * is ceo-recommender_amd/ceo_firm_matching/_native.py; INTEGRATION.md shows
+ * the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - every pointer argument is a DEVICE pointer owned by the caller (torch
+ *     tensors' data_ptr), fp32 row-major unless noted; descriptors
+ *     (tt_model_desc, tt_batch, tt_adam_hp) are HOST structs;
+ *   - no entry point allocates, synchronises or keeps global state; work is
+ *     enqueued on the given hipStream_t (so all of it is graph-capturable);
+ *   - return value: TT_OK or a negative TT_ERR_* (argument errors, detected
+ *     on the host before anything is enqueued) or a positive hipError_t.
+ */
+#ifndef CEO_TT_H
+#define CEO_TT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TT_ABI_VERSION 1
+#define TT_MAX_CAT 16      /* categorical columns per tower */
+
+/* status codes */
+#define TT_OK 0
+#define TT_ERR_ARG (-1)            /* bad pointer / size */
+#define TT_ERR_BATCH_TOO_SMALL (-2) /* train-mode BatchNorm needs B >= 2 (torch ValueError) */
+#define TT_ERR_UNSUPPORTED (-3)    /* shape outside what the fused kernels cover */
+#define TT_ERR_WORKSPACE (-4)      /* workspace too small */
+
+typedef struct ihipStream_t* tt_stream_t; /* == hipStream_t */
+
+/* Model geometry: CEOFirmMatcher(metadata, config)  (model.py:19-65).
+ * tower 0 = firm, tower 1 = ceo.  Fixed by the reference architecture:
+ * Linear(in,64) BN(64) ReLU Dropout Linear(64,32) BN(32) ReLU Dropout
+ * Linear(32,latent)  (model.py:37-62).                                       */
+typedef struct tt_model_desc {
+  int32_t n_num[2];                    /* metadata n_firm_numeric / n_ceo_numeric */
+  int32_t n_cat[2];                    /* len(firm_cat_counts) / len(ceo_cat_counts) */
+  int32_t emb_dim[2];                  /* EMBEDDING_DIM_LARGE (48) / _MEDIUM (8) */
+  int32_t latent;                      /* config.LATENT_DIM */
+  int32_t cat_counts[2][TT_MAX_CAT];   /* embedding rows per categorical column */
+  float dropout_p;                     /* nn.Dropout(0.1) */
+  float bn_eps;                        /* 1e-5 */
+  float bn_momentum;                   /* 0.1 */
+} tt_model_desc;
+
+/* One batch, described over dataset-resident arrays.  Row i of the batch is
+ * dataset row rows[row0 + i] (or row0 + i when rows == NULL).  With cycle > 0
+ * the offset comes from the device step counter instead (graph replay):
+ * row0 = ((t - 1 - t_base) % cycle) * n_rows.  Replaces the per-sample
+ * CEOFirmDataset.__getitem__ + collate + .to(DEVICE) (data.py:190-198,
+ * training.py:40-42).                                                        */
+typedef struct tt_batch {
+  const float* num[2];     int64_t num_ld[2];   /* firm_numeric / ceo_numeric [N, ld] */
+  const int64_t* cat[2];   int64_t cat_ld[2];   /* firm_cat / ceo_cat [N, ld] int64 */
+  const float* target;                          /* match_means [N] */
+  const float* weight;                          /* 1/(sd^2+1e-6) [N] */
+  const int64_t* rows;                          /* permutation / index list or NULL */
+  int64_t row0;
+  int64_t n_rows;                               /* B */
+  int64_t cycle;
+  int64_t t_base;
+} tt_batch;
+
+/* torch.optim.Adam defaults used by train_model (training.py:32) */
+typedef struct tt_adam_hp {
+  float lr, beta1, beta2, eps;
+} tt_adam_hp;
+
+/* Device-resident step counters (so a captured hipGraph can be replayed). */
+typedef struct tt_state {
+  int64_t step_done;   /* completed optimizer steps */
+  int64_t step_cur;    /* step being executed (written by the first kernel) */
+  float loss_sum;      /* += batch-mean weighted MSE of every step */
+  float pad0;
+  int64_t pad1;
+} tt_state;
+
+/* Slot ids for tt_param_offsets (float offsets into the flat parameter
+ * arena, which is laid out in CEOFirmMatcher.parameters() order). */
+enum {
+  TT_SLOT_W0 = 0, TT_SLOT_B0, TT_SLOT_G0, TT_SLOT_BE0,
+  TT_SLOT_W4, TT_SLOT_B4, TT_SLOT_G1, TT_SLOT_BE1, TT_SLOT_W8, TT_SLOT_B8,
+  TT_SLOTS_PER_TOWER
+};
+#define TT_NUM_OFFSETS (2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER + 1)
+/* out[0..15]   firm embedding tables,  out[16..31] ceo embedding tables,
+ * out[32..41]  firm tower slots,       out[42..51] ceo tower slots,
+ * out[52]      logit_scale.            (-1 for absent tables)            */
+
+int32_t tt_abi_version(void);
+
+/* Flat parameter arena size (floats) and per-parameter offsets. */
+int64_t tt_param_count(const tt_model_desc* d);
+int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out /* TT_NUM_OFFSETS */);
+/* BN running stats arena (floats): per tower running_mean0[64] running_var0[64]
+ * running_mean1[32] running_var1[32]; num_batches_tracked lives in a separate
+ * int64[4] array (firm bn1, firm bn5, ceo bn1, ceo bn5). */
+int64_t tt_buffer_count(const tt_model_desc* d);
+/* Bytes of the zero-initialised workspace for batches of up to max_batch. */
+int64_t tt_workspace_bytes(const tt_model_desc* d, int64_t max_batch);
+
+/* Forward of CEOFirmMatcher (model.py:67-89).  train=1: batch-statistics
+ * BatchNorm (+ running-stat update, model.py:39,43) and dropout drawn from the
+ * counter RNG stream (seed, step); train=0: running stats, no dropout.
+ * Writes score[B]; keeps what backward needs in ws.                        */
+int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, int64_t* nbt,
+                   const tt_batch* b, int32_t train, uint64_t seed, int64_t step,
+                   void* ws, int64_t ws_bytes, float* score, tt_stream_t stream);
+
+/* Backward of the preceding train-mode tt_forward on the same ws/batch/seed/
+ * step: autograd reverse of model.py:67-89 given dL/dscore (training.py:54).
+ * Writes the full flat gradient grad[param_count] (overwrites).             */
+int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch* b,
+                    const float* dscore, uint64_t seed, int64_t step,
+                    void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream);
+
+/* One fused training step = training.py:44-57: forward, weighted MSE,
+ * backward, and (apply_adam=1) the Adam update.  With apply_adam=0 only grad
+ * is produced (data-parallel: all-reduce grad, then tt_adam_apply).
+ * Dropout stream and Adam step t come from state (t = step_done + 1).       */
+int32_t tt_train_step(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
+                      const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state,
+                      void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
+                      int32_t apply_adam, tt_stream_t stream);
+
+/* tt_train_step with per-kernel timing: when events != NULL, events[k]
+ * (a hipEvent_t, or NULL to skip) is recorded on `stream` before kernel k of
+ * the step (k = 0..5: l0_fwd, l4_fwd, top, bwd_mid, bwd_first, reduce_adam)
+ * and events[6] after the last one.  Used by bench.py's roofline leg.       */
+int32_t tt_train_step_ev(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
+                         const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state,
+                         void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
+                         int32_t apply_adam, tt_stream_t stream, void* const* events);
+
+/* Adam over a flat arena (optim.Adam.step, training.py:55; torch 2.10
+ * _single_tensor_adam arithmetic).  step t = state->step_cur when state is
+ * not NULL (then state->step_done := t), else step_host.                    */
+int32_t tt_adam_apply(float* params, const float* grad, float* exp_avg, float* exp_avg_sq,
+                      int64_t n, const tt_adam_hp* hp, tt_state* state, int64_t step_host,
+                      tt_stream_t stream);
+
+/* Standalone fused L2-normalise + scaled cosine (+ weighted MSE fwd/bwd)
+ * over precomputed tower outputs u, v [B, D] (model.py:79-87,
+ * training.py:52).  score = exp(logit_scale) * <u/|u|, v/|v|>.
+ *   tt_cosine_forward : score only.
+ *   tt_cosine_mse_fwd_bwd : also loss_sum += sum w (s-t)^2 * inv_batch,
+ *     dls_sum += sum ds*score, du, dv  with ds = 2 w (s-t) * inv_batch.      */
+int32_t tt_cosine_forward(const float* u, const float* v, int64_t B, int32_t D,
+                          const float* logit_scale, float* score, tt_stream_t stream);
+int32_t tt_cosine_mse_fwd_bwd(const float* u, const float* v, const float* target,
+                              const float* weight, int64_t B, int32_t D,
+                              const float* logit_scale, float inv_batch, float* score,
+                              float* du, float* dv, float* loss_sum, float* dls_sum,
+                              tt_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CEO_TT_H */

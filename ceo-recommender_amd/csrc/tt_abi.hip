@@ -47,10 +47,11 @@ static Layout make_layout(const tt_model_desc* d) {
   int64_t off = 0;
   for (int t = 0; t < 2; ++t)
     for (int j = 0; j < TT_MAX_CAT; ++j) L.emb_off[t][j] = -1;
+  // every parameter starts on a 16-byte boundary (float4 loads of weights)
   for (int t = 0; t < 2; ++t)
     for (int j = 0; j < d->n_cat[t]; ++j) {
       L.emb_off[t][j] = off;
-      off += (int64_t)d->cat_counts[t][j] * d->emb_dim[t];
+      off = round_up(off + (int64_t)d->cat_counts[t][j] * d->emb_dim[t], 4);
     }
   const int D = d->latent;
   for (int t = 0; t < 2; ++t) {
@@ -61,7 +62,7 @@ static Layout make_layout(const tt_model_desc* d) {
                                             (int64_t)D * H1, D};
     for (int s = 0; s < TT_SLOTS_PER_TOWER; ++s) {
       L.slot[t][s] = off;
-      off += sz[s];
+      off = round_up(off + sz[s], 4);
     }
     int64_t so = 0;
     L.so[t][0] = so; so += (int64_t)H0 * in;
@@ -115,31 +116,39 @@ static std::once_flag g_attr_once;
 static void set_lds_attrs() {
   std::call_once(g_attr_once, [] {
     const int mx = (int)LDS_MAX;
-    (void)hipFuncSetAttribute((const void*)k_l0_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_l4_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_top<4>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_top<8>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_bwd_mid, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_bwd_first, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    const void* ks[] = {(const void*)k_l0_fwd<ROWS>,     (const void*)k_l4_fwd<ROWS>,
+                        (const void*)k_top<4, 64>,        (const void*)k_top<8, 64>,
+                        (const void*)k_top<4, 128>,       (const void*)k_top<8, 128>,
+                        (const void*)k_bwd_mid<ROWS>,    (const void*)k_bwd_first<ROWS>};
+    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   });
 }
 
 struct Plan {
   size_t lds_l0, lds_l4, lds_top, lds_mid, lds_first;
   int ndt;
+  int top_rows;     // row tile of k_top (64, or 128 for large batches)
+  int n_tiles;      // 64-row tiles
+  int n_tiles_top;  // k_top tiles
 };
 
-static int make_plan(const tt_model_desc* d, const Layout& L, Plan* P) {
+static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P) {
   if (d->latent > 128) return TT_ERR_UNSUPPORTED;
   P->ndt = d->latent <= 64 ? 4 : 8;
   const int kpm = std::max(L.kp[0], L.kp[1]);
   if (kpm > MAX_KP) return TT_ERR_UNSUPPORTED;
   const bool emb = d->n_cat[0] > 0 || d->n_cat[1] > 0;
-  P->lds_l0 = lds_l0_fwd(kpm);
-  P->lds_l4 = lds_l4_fwd();
-  P->lds_top = lds_top(P->ndt);
-  P->lds_mid = lds_bwd_mid();
-  P->lds_first = lds_bwd_first(kpm, emb);
+  // 128-row k_top tiles once the grid still covers every CU twice over
+  P->top_rows = B >= 16384 ? 128 : 64;
+  P->n_tiles = (int)((B + ROWS - 1) / ROWS);
+  P->n_tiles_top = (int)((B + P->top_rows - 1) / P->top_rows);
+  P->lds_l0 = L0Lds<ROWS>::bytes(kpm);
+  P->lds_l4 = L4Lds<ROWS>::bytes;
+  const int tl = P->ndt == 4 ? (P->top_rows == 64 ? TopLds<4, 64>::total : TopLds<4, 128>::total)
+                             : (P->top_rows == 64 ? TopLds<8, 64>::total : TopLds<8, 128>::total);
+  P->lds_top = sizeof(float) * (size_t)tl;
+  P->lds_mid = MidLds<ROWS>::bytes;
+  P->lds_first = FirstLds<ROWS>::bytes(kpm, emb);
   for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first})
     if (s > LDS_MAX) return TT_ERR_UNSUPPORTED;
   return TT_OK;
@@ -168,6 +177,8 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
     T.emb_dim = d->n_cat[t] > 0 ? d->emb_dim[t] : 1;
     T.in_dim = L.in_dim[t];
     T.kp = L.kp[t];
+    T.num_vec = d->n_cat[t] == 0 && d->n_num[t] % 4 == 0 && b->num_ld[t] % 4 == 0 &&
+                (uintptr_t)b->num[t] % 16 == 0;
     float* gacc = ws + W.gacc;
     for (int j = 0; j < d->n_cat[t]; ++j) {
       T.emb[j] = params + L.emb_off[t][j];
@@ -237,33 +248,37 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.g_ls = ws + W.gacc + L.ls;
 }
 
-static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout& W, float* ws, int n_slabs,
+// Segments of the parameter arena for k_reduce_adam: W/b ranges come from the
+// per-tile partial slabs (k_top writes n_tiles_top of them, the 64-row
+// kernels n_tiles), BN affine / embeddings / logit_scale from gacc.
+static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout& W, float* ws, const Plan& P,
                         float* grad) {
   RedArgs r;
   std::memset(&r, 0, sizeof(r));
   int k = 0;
-  auto add = [&](int64_t off, int64_t len, int kind, int tower, int64_t so) {
+  auto add = [&](int64_t off, int64_t len, int kind, int tower, int64_t so, int n_slabs) {
     if (len <= 0) return;
     r.seg[k].off = off;
     r.seg[k].len = len;
     r.seg[k].kind = kind;
     r.seg[k].tower = tower;
     r.seg[k].slab_off = so;
+    r.seg[k].n_slabs = n_slabs;
     ++k;
   };
   int64_t emb_total = L.slot[0][TT_SLOT_W0];
-  add(0, emb_total, 1, 0, 0);
+  add(0, emb_total, 1, 0, 0, 0);
   for (int t = 0; t < 2; ++t) {
     const int64_t* s = L.slot[t];
-    add(s[TT_SLOT_W0], s[TT_SLOT_G0] - s[TT_SLOT_W0], 0, t, L.so[t][0]);
-    add(s[TT_SLOT_G0], s[TT_SLOT_W4] - s[TT_SLOT_G0], 1, t, 0);
-    add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2]);
-    add(s[TT_SLOT_G1], s[TT_SLOT_W8] - s[TT_SLOT_G1], 1, t, 0);
-    add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], 0, t, L.so[t][4]);
+    add(s[TT_SLOT_W0], s[TT_SLOT_G0] - s[TT_SLOT_W0], 0, t, L.so[t][0], P.n_tiles);
+    add(s[TT_SLOT_G0], s[TT_SLOT_W4] - s[TT_SLOT_G0], 1, t, 0, 0);
+    add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles);
+    add(s[TT_SLOT_G1], s[TT_SLOT_W8] - s[TT_SLOT_G1], 1, t, 0, 0);
+    add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], 0, t, L.so[t][4], P.n_tiles_top);
   }
-  add(L.ls, 1, 1, 0, 0);
+  add(L.ls, 1, 1, 0, 0, 0);
   r.n_seg = k;
-  r.n_slabs = n_slabs;
+  r.n_slabs = P.n_tiles;
   r.n = L.n;
   r.slab[0] = ws + W.slab[0];
   r.slab[1] = ws + W.slab[1];
@@ -287,7 +302,7 @@ struct Ctx {
 static int prepare(const tt_model_desc* d, const tt_batch* b, int64_t ws_bytes, Ctx* c) {
   if (!desc_ok(d) || !batch_ok(d, b)) return TT_ERR_ARG;
   c->L = make_layout(d);
-  int rc = make_plan(d, c->L, &c->P);
+  int rc = make_plan(d, c->L, std::max<int64_t>(b->n_rows, 1), &c->P);
   if (rc) return rc;
   c->W = make_ws(c->L, std::max<int64_t>(b->n_rows, 1));
   if ((int64_t)(c->W.total * sizeof(float)) > ws_bytes) return TT_ERR_WORKSPACE;
@@ -295,12 +310,28 @@ static int prepare(const tt_model_desc* d, const tt_batch* b, int64_t ws_bytes, 
   return TT_OK;
 }
 
+static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s) {
+  hipLaunchKernelGGL(k_l0_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l0, s, a);
+}
+static void launch_l4(const StepArgs& a, const Plan& P, hipStream_t s) {
+  hipLaunchKernelGGL(k_l4_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l4, s, a);
+}
+static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s) {
+  hipLaunchKernelGGL(k_bwd_mid<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_mid, s, a);
+}
+static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s) {
+  hipLaunchKernelGGL(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, a);
+}
 static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s) {
-  const dim3 grid(a.n_tiles, grid_y);
-  if (P.ndt == 4)
-    hipLaunchKernelGGL(k_top<4>, grid, dim3(THREADS), P.lds_top, s, a);
+  const dim3 grid(P.n_tiles_top, grid_y), blk(4 * P.top_rows);
+  if (P.ndt == 4 && P.top_rows == 64)
+    hipLaunchKernelGGL((k_top<4, 64>), grid, blk, P.lds_top, s, a);
+  else if (P.ndt == 4)
+    hipLaunchKernelGGL((k_top<4, 128>), grid, blk, P.lds_top, s, a);
+  else if (P.top_rows == 64)
+    hipLaunchKernelGGL((k_top<8, 64>), grid, blk, P.lds_top, s, a);
   else
-    hipLaunchKernelGGL(k_top<8>, grid, dim3(THREADS), P.lds_top, s, a);
+    hipLaunchKernelGGL((k_top<8, 128>), grid, blk, P.lds_top, s, a);
 }
 
 }  // namespace tt
@@ -363,9 +394,8 @@ int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, 
       (void)hipMemsetAsync(w + c.W.st1[t], 0, sizeof(float) * 2 * H1, s);
     }
   }
-  const dim3 grid(a.n_tiles, 2);
-  hipLaunchKernelGGL(k_l0_fwd, grid, dim3(THREADS), c.P.lds_l0, s, a);
-  hipLaunchKernelGGL(k_l4_fwd, grid, dim3(THREADS), c.P.lds_l4, s, a);
+  launch_l0(a, c.P, s);
+  launch_l4(a, c.P, s);
   launch_top(a, c.P, 1, s);
   return launch_check();
 }
@@ -389,11 +419,10 @@ int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch*
   a.mode = TOP_BWD_GIVEN;
   a.dscore = dscore;
   (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
-  const dim3 grid(a.n_tiles, 2);
   launch_top(a, c.P, 2, s);
-  hipLaunchKernelGGL(k_bwd_mid, grid, dim3(THREADS), c.P.lds_mid, s, a);
-  hipLaunchKernelGGL(k_bwd_first, grid, dim3(THREADS), c.P.lds_first, s, a);
-  RedArgs r = make_red(d, c.L, c.W, w, a.n_tiles, grad);
+  launch_mid(a, c.P, s);
+  launch_first(a, c.P, s);
+  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   const int nb = (int)((c.L.n + RED_E - 1) / RED_E);
   hipLaunchKernelGGL(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, r);
   return launch_check();
@@ -420,22 +449,21 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   a.state = state;
   a.mode = TOP_TRAIN;
   a.loss_sum = &state->loss_sum;
-  const dim3 grid(a.n_tiles, 2);
   auto ev = [&](int k) {
     if (events && events[k]) (void)hipEventRecord((hipEvent_t)events[k], s);
   };
   ev(0);
-  hipLaunchKernelGGL(k_l0_fwd, grid, dim3(THREADS), c.P.lds_l0, s, a);
+  launch_l0(a, c.P, s);
   ev(1);
-  hipLaunchKernelGGL(k_l4_fwd, grid, dim3(THREADS), c.P.lds_l4, s, a);
+  launch_l4(a, c.P, s);
   ev(2);
   launch_top(a, c.P, 2, s);
   ev(3);
-  hipLaunchKernelGGL(k_bwd_mid, grid, dim3(THREADS), c.P.lds_mid, s, a);
+  launch_mid(a, c.P, s);
   ev(4);
-  hipLaunchKernelGGL(k_bwd_first, grid, dim3(THREADS), c.P.lds_first, s, a);
+  launch_first(a, c.P, s);
   ev(5);
-  RedArgs r = make_red(d, c.L, c.W, w, a.n_tiles, grad);
+  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   for (int t = 0; t < 2; ++t) {
     r.zero_buf[2 * t] = w + c.W.st0[t];
     r.zero_len[2 * t] = 2 * H0;

@@ -16,6 +16,7 @@ constexpr int H1 = 32;    // model.py:42  Linear(64, 32)
 constexpr int ROWS = 64;  // rows of the batch per row tile (one 16-row strip per wave)
 constexpr int WAVES = ROWS / 16;
 constexpr int THREADS = WAVES * WAVE;
+constexpr int TOP_ROWS_MAX = 128;  // k_top may use 128-row tiles (8 waves)
 constexpr int MAX_KP = 256;  // padded tower input width supported by the fused kernels
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -109,6 +110,7 @@ struct TowerDev {
   const float* num;  int64_t num_ld;      // numeric features [N, num_ld]
   const int64_t* cat; int64_t cat_ld;     // categorical codes [N, cat_ld]
   int n_num, n_cat, emb_dim, in_dim, kp;  // kp = in_dim rounded up to 16
+  int num_vec;                            // numeric rows 16-B aligned, no embeddings: float4 gather
   const float* emb[TT_MAX_CAT];           // embedding tables (param arena)
   int emb_rows[TT_MAX_CAT];               // rows per table (codes are clamped into range)
   float* gemb[TT_MAX_CAT];                // their gradient accumulators (gacc arena)
@@ -168,6 +170,112 @@ __device__ __forceinline__ int64_t data_row(const StepArgs& a, int64_t base, int
   return a.rows ? a.rows[base + i] : base + i;
 }
 
+// ---------------------------------------------------------------------------
+// Global -> LDS staging.  Every helper issues UNR independent 16-byte loads
+// per thread before the first LDS store (no per-iteration latency chain:
+// these kernels are latency-, not bandwidth-bound at B = 16K).
+// ---------------------------------------------------------------------------
+// g[R][C] (row stride gld floats) -> s[R][sld]; C % 4 == 0, 16-B aligned rows.
+template <int NT, int UNR>
+__device__ __forceinline__ void g2s_f4(const float* __restrict__ g, int64_t gld, float* s, int sld, int R, int C) {
+  const int c4 = C >> 2, n4 = R * c4;
+  for (int base = 0; base < n4; base += NT * UNR) {
+    float4 v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = min(base + (int)threadIdx.x + k * NT, n4 - 1);
+      const int r = e / c4, c = e - r * c4;
+      v[k] = *reinterpret_cast<const float4*>(g + r * gld + 4 * c);
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = base + (int)threadIdx.x + k * NT;
+      if (e < n4) {
+        const int r = e / c4, c = e - r * c4;
+        *reinterpret_cast<float4*>(s + r * sld + 4 * c) = v[k];
+      }
+    }
+  }
+}
+// transposed: g[R][C] -> s[C][sld] (s[c][r] = g[r][c]); C % 4 == 0.
+template <int NT, int UNR>
+__device__ __forceinline__ void g2s_f4_T(const float* __restrict__ g, int64_t gld, float* s, int sld, int R, int C) {
+  const int c4 = C >> 2, n4 = R * c4;
+  for (int base = 0; base < n4; base += NT * UNR) {
+    float4 v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = min(base + (int)threadIdx.x + k * NT, n4 - 1);
+      const int r = e / c4, c = e - r * c4;
+      v[k] = *reinterpret_cast<const float4*>(g + r * gld + 4 * c);
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = base + (int)threadIdx.x + k * NT;
+      if (e < n4) {
+        const int r = e / c4, c = 4 * (e - r * c4);
+        s[(c + 0) * sld + r] = v[k].x;
+        s[(c + 1) * sld + r] = v[k].y;
+        s[(c + 2) * sld + r] = v[k].z;
+        s[(c + 3) * sld + r] = v[k].w;
+      }
+    }
+  }
+}
+// scalar version for rows that are not 16-B aligned: g[R][C] -> s[R][sld]
+template <int NT, int UNR>
+__device__ __forceinline__ void g2s_f1(const float* __restrict__ g, int64_t gld, float* s, int sld, int R, int C) {
+  const int n = R * C;
+  for (int base = 0; base < n; base += NT * UNR) {
+    float v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = min(base + (int)threadIdx.x + k * NT, n - 1);
+      const int r = e / C, c = e - r * C;
+      v[k] = g[r * gld + c];
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = base + (int)threadIdx.x + k * NT;
+      if (e < n) {
+        const int r = e / C, c = e - r * C;
+        s[r * sld + c] = v[k];
+      }
+    }
+  }
+}
+template <int NT, int UNR>
+__device__ __forceinline__ void g2s_f1_T(const float* __restrict__ g, int64_t gld, float* s, int sld, int R, int C) {
+  const int n = R * C;
+  for (int base = 0; base < n; base += NT * UNR) {
+    float v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = min(base + (int)threadIdx.x + k * NT, n - 1);
+      const int r = e / C, c = e - r * C;
+      v[k] = g[r * gld + c];
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int e = base + (int)threadIdx.x + k * NT;
+      if (e < n) {
+        const int r = e / C, c = e - r * C;
+        s[c * sld + r] = v[k];
+      }
+    }
+  }
+}
+// zero s[R][c0..c1) (padding columns)
+template <int NT>
+__device__ __forceinline__ void zero_cols(float* s, int sld, int R, int c0, int c1) {
+  const int w = c1 - c0;
+  if (w <= 0) return;
+  for (int e = threadIdx.x; e < R * w; e += NT) {
+    const int r = e / w, c = e - r * w;
+    s[r * sld + c0 + c] = 0.f;
+  }
+}
+
 // X[row][col] of a tower input (numeric ++ embeddings), col < kp (zero pad)
 __device__ __forceinline__ float tower_x(const TowerDev& T, int64_t drow, int col) {
   if (col < T.n_num) return T.num[drow * T.num_ld + col];
@@ -190,6 +298,7 @@ struct Seg {
   int64_t off, len;      // range in the parameter arena
   int64_t slab_off;      // offset of the range inside a tower slab (kind 0)
   int32_t kind, tower;   // kind 0: slab partials, 1: atomic accumulator (gacc)
+  int32_t n_slabs, pad;  // partial slabs to sum (kind 0)
 };
 
 struct RedArgs {

@@ -51,8 +51,20 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
   if (si >= 0) {
     const Seg& S = a.seg[si];
     if (S.kind == 0) {
+      // fixed summation order (deterministic); UNR independent loads in flight
+      constexpr int UNR = 8;
       const float* base = a.slab[S.tower] + S.slab_off + (e - S.off);
-      for (int p = pg; p < a.n_slabs; p += RED_G) acc += base[(int64_t)p * a.slab_ld];
+      const int n = S.n_slabs;
+      for (int p0 = pg; p0 < n; p0 += RED_G * UNR) {
+        float v[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+          const int p = min(p0 + k * RED_G, n - 1);
+          v[k] = base[(int64_t)p * a.slab_ld];
+        }
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) acc += (p0 + k * RED_G < n) ? v[k] : 0.f;
+      }
     } else if (pg == 0) {
       acc = a.gacc[e];
     }

@@ -148,7 +148,8 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
                              : (P->top_rows == 64 ? TopLds<8, 64>::total : TopLds<8, 128>::total);
   P->lds_top = sizeof(float) * (size_t)tl;
   P->lds_mid = MidLds<ROWS>::bytes;
-  P->lds_first = FirstLds<ROWS>::bytes(kpm, emb);
+  P->lds_first = FirstLds<ROWS>::bytes(kpm);
+  (void)emb;
   for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first})
     if (s > LDS_MAX) return TT_ERR_UNSUPPORTED;
   return TT_OK;

@@ -59,6 +59,32 @@ __device__ __forceinline__ void strip_gemm_nt(const float* A, int lda, const flo
   }
 }
 
+// Strip GEMM with A given TRANSPOSED in LDS (AT[k][m], stride lda) and B given
+// row-major [k][n] (stride ldb); both read with 4 ds_read_b32 per operand:
+//   C[16 x 16*NT] = A[16 x K] * B[K x 16*NT],  A(r,k) = AT[k][r]
+template <int NT>
+__device__ __forceinline__ void strip_gemm_tn(const float* AT, int lda, const float* B, int ldb, int K,
+                                              f32x4 (&acc)[NT]) {
+  const int l = lane_id(), r = l & 15, g = l >> 4;
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    const float* ap = AT + (k0 + 4 * g) * lda + r;
+    const float4 a = make_float4(ap[0], ap[lda], ap[2 * lda], ap[3 * lda]);
+    const float* bp = B + (k0 + 4 * g) * ldb + r;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float4 b = make_float4(bp[16 * j], bp[ldb + 16 * j], bp[2 * ldb + 16 * j], bp[3 * ldb + 16 * j]);
+      mfma_k16(a, b, acc[j]);
+    }
+  }
+}
+
+// Store a C-layout 16x16 tile TRANSPOSED into LDS: dst[c][row0 + 4g .. +3]
+// (one ds_write_b128 per lane; dst row stride ld, row0 and ld multiples of 4)
+__device__ __forceinline__ void store_tile_T(float* dst, int ld, int c0, int row0, const f32x4& v) {
+  const int l = lane_id(), r = l & 15, g = l >> 4;
+  *reinterpret_cast<f32x4*>(dst + (c0 + r) * ld + row0 + 4 * g) = v;
+}
+
 // Rows-contracted product from C-layout registers (no LDS):
 //   acc[16 x 16] += P^T Q  over this wave's 16 rows, where P, Q are 16x16 tiles
 //   held in C layout (lane (r,g) holds rows 4g..4g+3 of column r).

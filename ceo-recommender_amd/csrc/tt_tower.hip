@@ -26,6 +26,8 @@
 // Latency discipline (B = 16K is a latency-bound size): every global load of
 // a phase is issued before its first use (batched 16-B loads, row indices
 // clamped instead of branched on), so one phase costs one memory round trip.
+#include <algorithm>
+
 #include "tt_common.h"
 
 namespace tt {
@@ -376,9 +378,10 @@ struct TopLds {
   static constexpr int W8s = 0;
   static constexpr int A1s = W8s + DP * LDA;
   static constexpr int Z4s = A1s + R * LDA;
-  static constexpr int dUs = Z4s + R * LDA;
-  static constexpr int dW8 = dUs + R * LDD;
-  static constexpr int db8 = dW8 + DP * H1;
+  static constexpr int LDT = R + 4;            // transposed images [col][row]
+  static constexpr int A1T = Z4s + R * LDA;    // [32][R+4]
+  static constexpr int dUT = A1T + H1 * LDT;   // [DP][R+4]
+  static constexpr int db8 = dUT + DP * LDT;
   static constexpr int cf1 = db8 + DP;
   static constexpr int red = cf1 + 2 * 4 * H1;
   static constexpr int scal = red + 2 * H1;  // [0] loss part [1] dls part
@@ -449,8 +452,8 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     cf[2 * H1 + c] = T.be1[c];
     cf[3 * H1 + c] = inv;
   }
-  for (int e = threadIdx.x; e < L::DP * H1 + L::DP; e += NTH) smem[L::dW8 + e] = 0.f;  // dW8 + db8
-  if (threadIdx.x < 2 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;                     // red + scal
+  if (threadIdx.x < L::DP) smem[L::db8 + threadIdx.x] = 0.f;
+  if (threadIdx.x < 2 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;  // red + scal
   stage_ridx<R>(a, base, r0, ridx);
   __syncthreads();
 
@@ -553,48 +556,60 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     }
   }
 
-  // own-tower output gradient in C layout (SURVEY 3D closed form)
+  // own-tower output gradient in C layout (SURVEY 3D closed form),
+  // d(own) = dc * (oth/|oth| - own * cos/|own|) / |own|
   f32x4 dO[NDT];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float dc = ds[i] * s;
+    const float ino = 1.f / no[i], int_ = 1.f / nt[i];
+    const float ka = valid[i] ? dc * ino * int_ : 0.f;
+    const float kb = valid[i] ? dc * cs[i] * ino * ino : 0.f;
 #pragma unroll
-    for (int j = 0; j < NDT; ++j)
-      dO[j][i] = valid[i] ? dc * (accO[j][i] / nt[i] - accS[j][i] * cs[i] / no[i]) / no[i] : 0.f;
+    for (int j = 0; j < NDT; ++j) dO[j][i] = ka * accO[j][i] - kb * accS[j][i];
   }
 
   const TowerDev& T = a.tw[own];
-  float* dUs = smem + L::dUs;
+  float* A1T = smem + L::A1T;
+  float* dUT = smem + L::dUT;
   const float* cf = smem + L::cf1 + own * 4 * H1;
   f32x4 a1[2], z4[2];
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < 2; ++q) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       a1[q][i] = A1s[(16 * w + 4 * g + i) * L::LDA + 16 * q + r];
       z4[q][i] = Z4s[(16 * w + 4 * g + i) * L::LDA + 16 * q + r];
     }
-
-  // dW8 (rows contracted straight from registers) and db8 -> LDS sums
+    store_tile_T(A1T, L::LDT, 16 * q, 16 * w, a1[q]);
+  }
+  // transposed dU image (one ds_write_b128 per tile) + db8 column sums
 #pragma unroll
   for (int j = 0; j < NDT; ++j) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      f32x4 acc = zero4();
-      cl_gemm_tn(dO[j], a1[q], acc);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(smem + L::dW8 + (16 * j + 4 * g + i) * H1 + 16 * q + r, acc[i]);
-    }
+    store_tile_T(dUT, L::LDT, 16 * j, 16 * w, dO[j]);
     const float cb = col_reduce(dO[j][0] + dO[j][1] + dO[j][2] + dO[j][3]);
     if (g == 0) atomicAdd(smem + L::db8 + 16 * j + r, cb);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dUs[(16 * w + 4 * g + i) * L::LDD + 16 * j + r] = dO[j][i];
   }
   __syncthreads();
 
-  // dA1 = dU W8  (W8s row-major [d][k] is the [K x N] operand)
+  // dW8 = dU^T A1 over all R rows of the tile: each wave owns whole output
+  // tiles (no cross-wave reduction) and stores them into this tile's slab.
+  float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
+  for (int p = w; p < NDT; p += R / 16) {
+    f32x4 acc[2] = {zero4(), zero4()};
+    strip_gemm_nt<2>(dUT + 16 * p * L::LDT, L::LDT, A1T, L::LDT, R, acc);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = 16 * p + 4 * g + i;
+        if (d < D) slab[T.so_W8 + d * H1 + 16 * q + r] = acc[q][i];
+      }
+  }
+
+  // dA1 = dU W8  (A from the transposed dU image, W8s row-major [d][k])
   f32x4 dA[2] = {zero4(), zero4()};
-  strip_gemm_nn<2>(dUs + 16 * w * L::LDD, L::LDD, W8s, L::LDA, L::DP, dA);
+  strip_gemm_tn<2>(dUT + 16 * w, L::LDT, W8s, L::LDA, L::DP, dA);
 
   // dY1 = dA1 * mask*scale * [Y1 > 0]  ==  [A1 > 0] * dA1 * scale
   const float scl = (a.drop_thr > 0) ? a.drop_scale : 1.f;
@@ -628,9 +643,6 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     atomicAdd(a.g_ls, smem[L::scal + 1]);
     if (a.mode == TOP_TRAIN && a.loss_sum) atomicAdd(a.loss_sum, smem[L::scal + 0] / (float)a.B);
   }
-  float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
-  for (int e = threadIdx.x; e < D * (H1 / 4); e += NTH)
-    reinterpret_cast<float4*>(slab + T.so_W8)[e] = reinterpret_cast<const float4*>(smem + L::dW8)[e];
   for (int e = threadIdx.x; e < D; e += NTH) slab[T.so_b8 + e] = smem[L::db8 + e];
 }
 
@@ -639,25 +651,27 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
 // ---------------------------------------------------------------------------
 template <int R>
 struct MidLds {
-  static constexpr int LD4 = H1 + 4;
+  static constexpr int LDW = H0 + 4;   // W4 row-major [32][68]
+  static constexpr int LDT = R + 4;    // transposed images [col][row]
   static constexpr size_t bytes =
-      sizeof(float) * ((size_t)(H0 + R) * LD4 + H1 * H0 + H1 + 5 * H1 + 4 * H0 + 2 * H0);
+      sizeof(float) * ((size_t)H1 * LDW + (size_t)(H1 + H0) * LDT + H1 + 5 * H1 + 4 * H0 + 2 * H0);
 };
 
 template <int R>
 __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
+  static_assert(R == 64, "dW4 tile ownership assumes 4 waves");
   constexpr int NTH = R * 4;
-  constexpr int LD4 = MidLds<R>::LD4;
+  constexpr int LDW = MidLds<R>::LDW, LDT = MidLds<R>::LDT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
   const TowerDev& T = a.tw[t];
   const int64_t step = step_current(a);
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  float* W4Ts = smem;                 // [64][36]  W4^T
-  float* dZs = W4Ts + H0 * LD4;       // [R][36]
-  float* dW4 = dZs + R * LD4;         // [32][64]
-  float* db4 = dW4 + H1 * H0;         // [32]
+  float* W4s = smem;                  // [32][68]  W4 row-major
+  float* dZT = W4s + H1 * LDW;        // [32][R+4] dZ4^T
+  float* A0T = dZT + H1 * LDT;        // [64][R+4] A0^T
+  float* db4 = A0T + H0 * LDT;        // [32]
   float* c1 = db4 + H1;               // k1[32] mb[32] mg[32] mean1[32] inv1[32]
   float* c0 = c1 + 5 * H1;            // mean0[64] alpha0[64] beta0[64] inv0[64]
   float* red = c0 + 4 * H0;           // [128]
@@ -692,12 +706,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     c0[2 * H0 + c] = T.be0[c];
     c0[3 * H0 + c] = inv;
   }
-  for (int e = threadIdx.x; e < H1 * H0 + H1; e += NTH) dW4[e] = 0.f;
+  if (threadIdx.x < H1) db4[threadIdx.x] = 0.f;
   if (threadIdx.x < 2 * H0) red[threadIdx.x] = 0.f;
-  g2s_f4_T<NTH, 2>(T.W4, H0, W4Ts, LD4, H1, H0);
+  g2s_f4<NTH, 2>(T.W4, H0, W4s, LDW, H1, H0);
   __syncthreads();
 
-  // dZ4 in C layout (2 tiles)
+  // dZ4 (BN1 backward) and the recomputed A0 / normalised Z0, all C layout;
+  // transposed images for the rows-contracted dW4 product
   f32x4 dz[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -708,10 +723,11 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
       const float zh = (zz4[q][i] - c1[3 * H1 + col]) * c1[4 * H1 + col];
       const float v = c1[col] * (dy1[q][i] - c1[H1 + col] - zh * c1[2 * H1 + col]);
       dz[q][i] = row < a.B ? v : 0.f;
-      dZs[(16 * w + 4 * g + i) * LD4 + col] = dz[q][i];
     }
+    store_tile_T(dZT, LDT, 16 * q, 16 * w, dz[q]);
+    const float cb = col_reduce(dz[q][0] + dz[q][1] + dz[q][2] + dz[q][3]);
+    if (g == 0) atomicAdd(db4 + col, cb);
   }
-  // A0 (recomputed) and the normalised Z0 in C layout (4 tiles)
   const bool drop = a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
   f32x4 a0[4], zh0[4];
@@ -728,25 +744,26 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
                     : 0.f;
       zh0[j][i] = ok ? (z - c0[col]) * c0[3 * H0 + col] : 0.f;
     }
-  }
-  // dW4 = dZ4^T A0 ; db4
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f32x4 acc = zero4();
-      cl_gemm_tn(dz[q], a0[j], acc);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(dW4 + (16 * q + 4 * g + i) * H0 + 16 * j + r, acc[i]);
-    }
-    const float cb = col_reduce(dz[q][0] + dz[q][1] + dz[q][2] + dz[q][3]);
-    if (g == 0) atomicAdd(db4 + 16 * q + r, cb);
+    store_tile_T(A0T, LDT, 16 * j, 16 * w, a0[j]);
   }
   __syncthreads();
 
-  // dA0 = dZ4 W4  (K = 32)
+  // dW4 = dZ4^T A0 over the tile's rows: wave w owns h1-tile (w&1) x h0-tiles
+  // 2*(w>>1)..+1 and writes them straight into this tile's slab
+  float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
+  {
+    const int p = w & 1, q0 = 2 * (w >> 1);
+    f32x4 acc[2] = {zero4(), zero4()};
+    strip_gemm_nt<2>(dZT + 16 * p * LDT, LDT, A0T + 16 * q0 * LDT, LDT, R, acc);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) slab[T.so_W4 + (16 * p + 4 * g + i) * H0 + 16 * (q0 + q) + r] = acc[q][i];
+  }
+
+  // dA0 = dZ4 W4  (K = 32; A from the transposed image, W4 row-major)
   f32x4 dA[4] = {zero4(), zero4(), zero4(), zero4()};
-  strip_gemm_nt<4>(dZs + 16 * w * LD4, LD4, W4Ts, LD4, H1, dA);
+  strip_gemm_tn<4>(dZT + 16 * w, LDT, W4s, LDW, H1, dA);
   const float scl = drop ? a.drop_scale : 1.f;
   float sg[4], sb[4];
 #pragma unroll
@@ -772,9 +789,6 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     atomicAdd(&T.gg0[threadIdx.x], red[threadIdx.x]);
     atomicAdd(&T.gbe0[threadIdx.x], red[H0 + threadIdx.x]);
   }
-  float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
-  for (int e = threadIdx.x; e < H1 * H0 / 4; e += NTH)
-    reinterpret_cast<float4*>(slab + T.so_W4)[e] = reinterpret_cast<const float4*>(dW4)[e];
   if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = db4[threadIdx.x];
 }
 
@@ -783,18 +797,22 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
 // ---------------------------------------------------------------------------
 template <int R>
 struct FirstLds {
-  static size_t bytes(int kp, bool emb) {
-    // Xs [R][kp+4] is reused for W0 [64][kp+4] by the embedding pass (R == 64)
-    size_t n = (size_t)H0 * kp + H0 + 5 * H0 + (size_t)std::max(R, H0) * (kp + 4) + 2 * R;
-    if (emb) n += (size_t)R * (H0 + 4);
-    return sizeof(float) * n;
+  static constexpr int LDT = R + 4;
+  // XT [kp][R+4] (X^T; reused as W0 [64][kp+4] by the embedding pass) | dZT [64][R+4]
+  __host__ __device__ static size_t xt_floats(int kp) {
+    const size_t a = (size_t)kp * LDT, b = (size_t)H0 * (kp + 4);
+    return a > b ? a : b;
+  }
+  static size_t bytes(int kp) {
+    return sizeof(float) * (xt_floats(kp) + (size_t)H0 * LDT + H0 + 5 * H0 + 2 * R);
   }
 };
 
 template <int R>
 __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
+  static_assert(R == 64, "dW0 tile ownership assumes 4 waves (one per 16 outputs of 64)");
   constexpr int NTH = R * 4;
-  constexpr int LD0 = H0 + 4;
+  constexpr int LDT = FirstLds<R>::LDT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
   const TowerDev& T = a.tw[t];
@@ -802,14 +820,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   const int64_t base = batch_row0(a, step);
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  const int kp = T.kp, ldk = kp + 4;
+  const int kp = T.kp, ldk = kp + 4, KT = kp / 16;
   const bool emb = T.n_cat > 0;
   int64_t* ridx = reinterpret_cast<int64_t*>(smem);  // [R]
-  float* dW0 = smem + 2 * R;         // [64][kp]
-  float* db0 = dW0 + H0 * kp;        // [64]
-  float* c0 = db0 + H0;              // k0[64] mb[64] mg[64] mean0[64] inv0[64]
-  float* Xs = c0 + 5 * H0;           // [R][ldk]; later W0 [64][ldk] (embedding pass)
-  float* dZs = Xs + (R > H0 ? R : H0) * ldk;  // [R][68]   (only with embeddings)
+  float* XT = smem + 2 * R;                            // [kp][R+4]
+  float* dZT = XT + FirstLds<R>::xt_floats(kp);        // [64][R+4]
+  float* db0 = dZT + H0 * LDT;                         // [64]
+  float* c0 = db0 + H0;                                // k0[64] mb[64] mg[64] mean0[64] inv0[64]
 
   f32x4 dy0[4], zz0[4];
 #pragma unroll
@@ -831,11 +848,55 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     c0[2 * H0 + c] = T.gg0[c] * invB;
     c0[3 * H0 + c] = T.fin0[c];
     c0[4 * H0 + c] = inv;
+    db0[c] = 0.f;
   }
-  for (int e = threadIdx.x; e < H0 * kp + H0; e += NTH) dW0[e] = 0.f;
   __syncthreads();
-  stage_x<R, NTH>(T, ridx, Xs, ldk);
 
+  // X^T tile: consecutive threads take consecutive rows (conflict-free LDS
+  // writes); gathered 16-B row loads, all issued before the stores
+  if (T.num_vec) {
+    const int c4n = T.n_num >> 2, n4 = R * c4n;
+    constexpr int UNR = 4;
+    for (int b0 = 0; b0 < n4; b0 += NTH * UNR) {
+      float4 v[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = min(b0 + (int)threadIdx.x + k * NTH, n4 - 1);
+        const int rr = e % R, c4 = e / R;
+        v[k] = *reinterpret_cast<const float4*>(T.num + ridx[rr] * T.num_ld + 4 * c4);
+      }
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = b0 + (int)threadIdx.x + k * NTH;
+        if (e < n4) {
+          const int rr = e % R, c = 4 * (e / R);
+          XT[(c + 0) * LDT + rr] = v[k].x;
+          XT[(c + 1) * LDT + rr] = v[k].y;
+          XT[(c + 2) * LDT + rr] = v[k].z;
+          XT[(c + 3) * LDT + rr] = v[k].w;
+        }
+      }
+    }
+    for (int e = threadIdx.x; e < (kp - T.n_num) * R; e += NTH) XT[(T.n_num + e / R) * LDT + e % R] = 0.f;
+  } else {
+    constexpr int UNR = 8;
+    const int n = R * kp;
+    for (int b0 = 0; b0 < n; b0 += NTH * UNR) {
+      float v[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = min(b0 + (int)threadIdx.x + k * NTH, n - 1);
+        v[k] = tower_x(T, ridx[e % R], e / R);
+      }
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = b0 + (int)threadIdx.x + k * NTH;
+        if (e < n) XT[(e / R) * LDT + e % R] = v[k];
+      }
+    }
+  }
+
+  // dZ0 (BN0 backward), C layout -> transposed image; db0 column sums
   f32x4 dz[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -846,37 +907,47 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
       const float zh = (zz0[j][i] - c0[3 * H0 + col]) * c0[4 * H0 + col];
       const float v = c0[col] * (dy0[j][i] - c0[H0 + col] - zh * c0[2 * H0 + col]);
       dz[j][i] = row < a.B ? v : 0.f;
-      if (emb) dZs[(16 * w + 4 * g + i) * LD0 + col] = dz[j][i];
     }
+    store_tile_T(dZT, LDT, 16 * j, 16 * w, dz[j]);
     const float cb = col_reduce(dz[j][0] + dz[j][1] + dz[j][2] + dz[j][3]);
     if (g == 0) atomicAdd(db0 + col, cb);
   }
   __syncthreads();
-  // dW0 = dZ0^T X, one 16-column tile of X at a time (X in C layout from LDS)
-  for (int kt = 0; kt < kp / 16; ++kt) {
-    f32x4 x;
+
+  // dW0 = dZ0^T X over the tile's rows: wave w owns outputs 16w..16w+15 and
+  // every input column tile; results go straight into this tile's slab
+  float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
+  const int in = T.in_dim;
+  auto put_w0 = [&](int kt, const f32x4& acc) {
+    const int k = 16 * kt + r;
+    if (k < in) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = Xs[(16 * w + 4 * g + i) * ldk + 16 * kt + r];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f32x4 acc = zero4();
-      cl_gemm_tn(dz[j], x, acc);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(dW0 + (16 * j + 4 * g + i) * kp + 16 * kt + r, acc[i]);
+      for (int i = 0; i < 4; ++i) slab[T.so_W0 + (16 * w + 4 * g + i) * in + k] = acc[i];
     }
+  };
+  int kt = 0;
+  for (; kt + 4 <= KT; kt += 4) {
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+    strip_gemm_nt<4>(dZT + 16 * w * LDT, LDT, XT + 16 * kt * LDT, LDT, R, acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) put_w0(kt + q, acc[q]);
+  }
+  for (; kt < KT; ++kt) {
+    f32x4 acc[1] = {zero4()};
+    strip_gemm_nt<1>(dZT + 16 * w * LDT, LDT, XT + 16 * kt * LDT, LDT, R, acc);
+    put_w0(kt, acc[0]);
   }
   if (emb) {
     // dX = dZ0 W0 on the embedding columns -> scatter-add into the tables.
-    // W0 (row-major [64][ldk]) takes over the X tile's LDS.
+    // W0 (row-major [64][ldk]) takes over the X^T image's LDS.
     __syncthreads();
-    float* W0s = Xs;
+    float* W0s = XT;
     stage_w<NTH>(T.W0, H0, T.in_dim, kp, W0s, ldk);
     __syncthreads();
-    const int kt0 = T.n_num / 16;
-    for (int kt = kt0; kt < kp / 16; ++kt) {
+    for (int ktt = T.n_num / 16; ktt < KT; ++ktt) {
       f32x4 dx[1] = {zero4()};
-      strip_gemm_nn<1>(dZs + 16 * w * LD0, LD0, W0s + 16 * kt, ldk, H0, dx);
-      const int col = 16 * kt + r;
+      strip_gemm_tn<1>(dZT + 16 * w, LDT, W0s + 16 * ktt, ldk, H0, dx);
+      const int col = 16 * ktt + r;
       if (col >= T.n_num && col < T.in_dim) {
         const int c = col - T.n_num;
         const int jj = c / T.emb_dim, e = c - jj * T.emb_dim;
@@ -890,13 +961,6 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
         }
       }
     }
-  }
-  __syncthreads();
-  float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
-  const int in = T.in_dim;
-  for (int e = threadIdx.x; e < H0 * in; e += NTH) {
-    const int n = e / in, k = e - n * in;
-    slab[T.so_W0 + e] = dW0[n * kp + k];
   }
   if (threadIdx.x < H0) slab[T.so_b0 + threadIdx.x] = db0[threadIdx.x];
 }

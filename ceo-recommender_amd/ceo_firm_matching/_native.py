@@ -26,7 +26,8 @@ TT_ERR_UNSUPPORTED = -3
 TT_ERR_WORKSPACE = -4
 
 _PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_PARENT, "lib", "libceo_tt.so")
+# CEO_TT_LIB: diagnostic override (e.g. the -DTT_STAMPS build); the in-tree library otherwise
+LIB_PATH = os.environ.get("CEO_TT_LIB") or os.path.join(_PKG_PARENT, "lib", "libceo_tt.so")
 EXPORTED = ("tt_abi_version", "tt_param_count", "tt_param_offsets", "tt_buffer_count",
             "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_train_step", "tt_train_step_ev",
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd")

@@ -10,6 +10,15 @@
 #include "tt_optim.hip"
 #include "tt_cosine.hip"
 
+#ifdef TT_STAMPS
+namespace tt {
+__device__ uint64_t* g_tt_stamps = nullptr;
+}
+extern "C" int32_t tt_debug_set_stamps(uint64_t* buf) {
+  return (int32_t)hipMemcpyToSymbol(HIP_SYMBOL(tt::g_tt_stamps), &buf, sizeof(buf));
+}
+#endif
+
 namespace tt {
 
 constexpr size_t LDS_MAX = 160 * 1024;
@@ -80,22 +89,28 @@ static Layout make_layout(const tt_model_desc* d) {
 
 struct WsLayout {
   int64_t Z0[2], Z4[2], dY0[2], dY1[2], st0[2], st1[2], sh0[2], sh1[2], fin0[2], fin1[2];
+  int64_t tgw;
   int64_t slab[2];
   int64_t gacc;
   int64_t total;  // floats
   int n_tiles;
 };
 
+// Per-row workspace arrays hold whole 128-row tiles (the kernels store rows
+// beyond B unconditionally into this padding instead of branching per row).
+static int64_t padded_rows(int64_t b) { return round_up(std::max<int64_t>(b, 1), TOP_ROWS_MAX); }
+
 static WsLayout make_ws(const Layout& L, int64_t max_batch) {
   WsLayout W;
   int64_t off = 0;
   auto take = [&](int64_t n) { const int64_t o = off; off += round_up(n, 64); return o; };
-  W.n_tiles = (int)((max_batch + ROWS - 1) / ROWS);
+  const int64_t rows = padded_rows(max_batch);
+  W.n_tiles = (int)(rows / ROWS);
   for (int t = 0; t < 2; ++t) {
-    W.Z0[t] = take(max_batch * H0);
-    W.Z4[t] = take(max_batch * H1);
-    W.dY0[t] = take(max_batch * H0);
-    W.dY1[t] = take(max_batch * H1);
+    W.Z0[t] = take(rows * H0);
+    W.Z4[t] = take(rows * H1);
+    W.dY0[t] = take(rows * H0);
+    W.dY1[t] = take(rows * H1);
     W.st0[t] = take(2 * H0);
     W.st1[t] = take(2 * H1);
     W.sh0[t] = take(H0);
@@ -103,6 +118,7 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
     W.fin0[t] = take(2 * H0);
     W.fin1[t] = take(2 * H1);
   }
+  W.tgw = take(rows * 2);
   for (int t = 0; t < 2; ++t) W.slab[t] = take((int64_t)W.n_tiles * L.slab_ld);
   W.gacc = take(L.n);
   W.total = off;
@@ -140,8 +156,10 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   const bool emb = d->n_cat[0] > 0 || d->n_cat[1] > 0;
   // 128-row k_top tiles once the grid still covers every CU twice over
   P->top_rows = B >= 16384 ? 128 : 64;
-  P->n_tiles = (int)((B + ROWS - 1) / ROWS);
-  P->n_tiles_top = (int)((B + P->top_rows - 1) / P->top_rows);
+  // the 64-row kernels cover the padded rows, so every workspace row that any
+  // kernel reads was written earlier in the same step
+  P->n_tiles = (int)(padded_rows(B) / ROWS);
+  P->n_tiles_top = (int)((P->n_tiles * ROWS) / P->top_rows);
   P->lds_l0 = L0Lds<ROWS>::bytes(kpm);
   P->lds_l4 = L4Lds<ROWS>::bytes;
   const int tl = P->ndt == 4 ? (P->top_rows == 64 ? TopLds<4, 64>::total : TopLds<4, 128>::total)
@@ -247,6 +265,7 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.slab_ld = (int)L.slab_ld;
   a.logit_scale = params + L.ls;
   a.g_ls = ws + W.gacc + L.ls;
+  a.tgw = ws + W.tgw;
 }
 
 // Segments of the parameter arena for k_reduce_adam: W/b ranges come from the

@@ -179,7 +179,24 @@ struct StepArgs {
   float* score;          // [B] output scores (nullable)
   const float* dscore;   // [B] upstream grad (TOP_BWD_GIVEN)
   float* loss_sum;       // [1] += sum w (s-t)^2 / B   (TOP_TRAIN)
+  float* tgw;            // [Bpad][2] (target, weight) of each batch row, gathered by k_l0_fwd
 };
+
+// ---------------------------------------------------------------------------
+// Diagnostic phase stamps (separate -DTT_STAMPS build only; compiled out of
+// the product library).  s_memrealtime (100 MHz, chip-wide) per block/phase.
+// ---------------------------------------------------------------------------
+#ifdef TT_STAMPS
+extern __device__ uint64_t* g_tt_stamps;
+#define TT_STAMP(kid, slot)                                                                             \
+  do {                                                                                                  \
+    if (g_tt_stamps && threadIdx.x == 0)                                                                \
+      g_tt_stamps[((uint64_t)(kid) * 2048 + blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] =        \
+          __builtin_amdgcn_s_memrealtime();                                                             \
+  } while (0)
+#else
+#define TT_STAMP(kid, slot) ((void)0)
+#endif
 
 __device__ __forceinline__ int64_t step_for_first_kernel(const StepArgs& a) {
   return a.state ? a.state->step_done + 1 : a.step_host;
@@ -202,9 +219,31 @@ __device__ __forceinline__ int64_t data_row(const StepArgs& a, int64_t base, int
 // these kernels are latency-, not bandwidth-bound at B = 16K).
 // ---------------------------------------------------------------------------
 // g[R][C] (row stride gld floats) -> s[R][sld]; C % 4 == 0, 16-B aligned rows.
+// When the element count is a multiple of NT*UNR (the usual shapes) the loop
+// has no per-element guard: a guarded store per element splits the code into
+// small basic blocks at whose joins hipcc drains vmcnt(0), serialising the
+// loads.  (Same rule for every hot loop in these kernels.)
 template <int NT, int UNR>
 __device__ __forceinline__ void g2s_f4(const float* __restrict__ g, int64_t gld, float* s, int sld, int R, int C) {
   const int c4 = C >> 2, n4 = R * c4;
+  if (n4 % (NT * UNR) == 0) {
+    for (int base = 0; base < n4; base += NT * UNR) {
+      float4 v[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = base + (int)threadIdx.x + k * NT;
+        const int r = e / c4, c = e - r * c4;
+        v[k] = *reinterpret_cast<const float4*>(g + r * gld + 4 * c);
+      }
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = base + (int)threadIdx.x + k * NT;
+        const int r = e / c4, c = e - r * c4;
+        *reinterpret_cast<float4*>(s + r * sld + 4 * c) = v[k];
+      }
+    }
+    return;
+  }
   for (int base = 0; base < n4; base += NT * UNR) {
     float4 v[UNR];
 #pragma unroll
@@ -227,6 +266,27 @@ __device__ __forceinline__ void g2s_f4(const float* __restrict__ g, int64_t gld,
 template <int NT, int UNR>
 __device__ __forceinline__ void g2s_f4_T(const float* __restrict__ g, int64_t gld, float* s, int sld, int R, int C) {
   const int c4 = C >> 2, n4 = R * c4;
+  if (n4 % (NT * UNR) == 0) {
+    for (int base = 0; base < n4; base += NT * UNR) {
+      float4 v[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = base + (int)threadIdx.x + k * NT;
+        const int r = e / c4, c = e - r * c4;
+        v[k] = *reinterpret_cast<const float4*>(g + r * gld + 4 * c);
+      }
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int e = base + (int)threadIdx.x + k * NT;
+        const int r = e / c4, c = 4 * (e - r * c4);
+        s[(c + 0) * sld + r] = v[k].x;
+        s[(c + 1) * sld + r] = v[k].y;
+        s[(c + 2) * sld + r] = v[k].z;
+        s[(c + 3) * sld + r] = v[k].w;
+      }
+    }
+    return;
+  }
   for (int base = 0; base < n4; base += NT * UNR) {
     float4 v[UNR];
 #pragma unroll

@@ -41,6 +41,7 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 
 __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
   __shared__ float part[RED_G][RED_E];
+  TT_STAMP(5, 0);
   const int el = threadIdx.x & (RED_E - 1), pg = threadIdx.x / RED_E;
   const int64_t e = (int64_t)blockIdx.x * RED_E + el;
   int si = -1;
@@ -75,6 +76,7 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
     for (int b = 0; b < 4; ++b)
       for (int i = threadIdx.x; i < a.zero_len[b]; i += blockDim.x) a.zero_buf[b][i] = 0.f;
   __syncthreads();
+  TT_STAMP(5, 1);
   if (pg != 0 || si < 0) return;
   float gsum = 0.f;
 #pragma unroll

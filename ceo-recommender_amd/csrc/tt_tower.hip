@@ -19,15 +19,18 @@
 //   k_bwd_first dZ0 (BN0 backward); dW0, db0; dX -> embedding grads (K1 bwd)
 //
 // GEMMs run on v_mfma_f32_16x16x4_f32 (exact fp32).  Row-wise products
-// (X W^T, dZ W) read both operands from LDS with ds_read_b128; the
-// row-contracted weight-gradient products (dZ^T X) take their operands
-// straight from the MFMA accumulator layout (tt_common.h cl_gemm_tn).
+// (X W^T, dZ W) read LDS operands (ds_read_b128 where the layout allows); the
+// row-contracted weight-gradient products (dZ^T X) are owned tile-by-tile by
+// the waves and read transposed LDS images written straight from the MFMA
+// accumulator layout (one ds_write_b128 per 16x16 tile).
 //
-// Latency discipline (B = 16K is a latency-bound size): every global load of
-// a phase is issued before its first use (batched 16-B loads, row indices
-// clamped instead of branched on), so one phase costs one memory round trip.
-#include <algorithm>
-
+// Latency discipline (B = 16K is a latency-bound size):
+//  * every global load of a phase is issued before its first use (batched
+//    16-B loads, small parameters prefetched at kernel entry);
+//  * no per-element guards around memory operations on the hot path: hipcc
+//    drains vmcnt(0) at every join of such guards.  Row indices are clamped
+//    for loads, the workspace is padded to whole tiles so per-row stores need
+//    no guard, and rows beyond B are masked out of statistics with selects.
 #include "tt_common.h"
 
 namespace tt {
@@ -103,20 +106,38 @@ __device__ __forceinline__ void stage_x(const TowerDev& T, const int64_t* ridx, 
   if (T.num_vec) {
     const int c4 = T.n_num >> 2, n4 = R * c4;
     constexpr int UNR = 4;
-    for (int base = 0; base < n4; base += NTH * UNR) {
-      float4 v[UNR];
+    if (n4 % (NTH * UNR) == 0) {
+      for (int base = 0; base < n4; base += NTH * UNR) {
+        float4 v[UNR];
 #pragma unroll
-      for (int k = 0; k < UNR; ++k) {
-        const int e = min(base + (int)threadIdx.x + k * NTH, n4 - 1);
-        const int r = e / c4, c = e - r * c4;
-        v[k] = *reinterpret_cast<const float4*>(T.num + ridx[r] * T.num_ld + 4 * c);
-      }
+        for (int k = 0; k < UNR; ++k) {
+          const int e = base + (int)threadIdx.x + k * NTH;
+          const int r = e / c4, c = e - r * c4;
+          v[k] = *reinterpret_cast<const float4*>(T.num + ridx[r] * T.num_ld + 4 * c);
+        }
 #pragma unroll
-      for (int k = 0; k < UNR; ++k) {
-        const int e = base + (int)threadIdx.x + k * NTH;
-        if (e < n4) {
+        for (int k = 0; k < UNR; ++k) {
+          const int e = base + (int)threadIdx.x + k * NTH;
           const int r = e / c4, c = e - r * c4;
           *reinterpret_cast<float4*>(Xs + r * ldk + 4 * c) = v[k];
+        }
+      }
+    } else {
+      for (int base = 0; base < n4; base += NTH * UNR) {
+        float4 v[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+          const int e = min(base + (int)threadIdx.x + k * NTH, n4 - 1);
+          const int r = e / c4, c = e - r * c4;
+          v[k] = *reinterpret_cast<const float4*>(T.num + ridx[r] * T.num_ld + 4 * c);
+        }
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+          const int e = base + (int)threadIdx.x + k * NTH;
+          if (e < n4) {
+            const int r = e / c4, c = e - r * c4;
+            *reinterpret_cast<float4*>(Xs + r * ldk + 4 * c) = v[k];
+          }
         }
       }
     }
@@ -154,31 +175,32 @@ __device__ __forceinline__ void stage_w(const float* W, int N, int K, int Kp, fl
   zero_cols<NTH>(s, ld, N, K, Kp);
 }
 
-// Strip GEMM with A row-major in LDS (b128) and B given ROW-MAJOR as [k][n]
-// (so B_nt[n][k] = B[k][n] is read with 4 ds_read_b32):
-//   C[16 x 16*NT] = A[16 x K] * B[K x 16*NT]
-template <int NT>
-__device__ __forceinline__ void strip_gemm_nn(const float* A, int lda, const float* B, int ldb, int K,
-                                              f32x4 (&acc)[NT]) {
-  const int l = lane_id(), r = l & 15, g = l >> 4;
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    const float4 a = *reinterpret_cast<const float4*>(A + r * lda + k0 + 4 * g);
-    const float* b0 = B + (k0 + 4 * g) * ldb + r;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const float4 b = make_float4(b0[16 * j], b0[ldb + 16 * j], b0[2 * ldb + 16 * j], b0[3 * ldb + 16 * j]);
-      mfma_k16(a, b, acc[j]);
-    }
+// Block-parallel dot products  out[c] = bias[c] + sum_k x[k] * W[c][k]  for
+// c < C (C*4 <= NTH): 4 threads per output, fixed summation order (so every
+// block computes bitwise the same value).  `part` is LDS scratch [4][C].
+template <int NTH>
+__device__ __forceinline__ void row_dot(const float* x, const float* W, int ld, int K, int C, const float* bias,
+                                        float* part, float* out) {
+  const int c = threadIdx.x % C, q = threadIdx.x / C;
+  if (q < 4) {
+    const int k0 = (K * q) / 4, k1 = (K * (q + 1)) / 4;
+    float z = 0.f;
+    for (int k = k0; k < k1; ++k) z = fmaf(x[k], W[c * ld + k], z);
+    part[q * C + c] = z;
   }
+  __syncthreads();
+  if (threadIdx.x < C) out[threadIdx.x] = ((part[threadIdx.x] + part[C + threadIdx.x]) +
+                                           (part[2 * C + threadIdx.x] + part[3 * C + threadIdx.x])) +
+                                          bias[threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------
-// k_l0_fwd : Z0 = X W0^T + b0 ; BN0 shifted moment sums
+// k_l0_fwd : Z0 = X W0^T + b0 ; BN0 shifted moment sums ; (target, weight)
 // ---------------------------------------------------------------------------
 template <int R>
 struct L0Lds {
   static size_t bytes(int kp) {
-    return sizeof(float) * ((size_t)(H0 + R) * (kp + 4) + 2 * H0 + H0 + kp) + sizeof(int64_t) * R;
+    return sizeof(float) * ((size_t)(H0 + R) * (kp + 4) + 2 * H0 + H0 + kp + 4 * H0) + sizeof(int64_t) * R;
   }
 };
 
@@ -192,13 +214,19 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
   const int64_t base = batch_row0(a, step);
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int kp = T.kp, ldk = kp + 4;
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   int64_t* ridx = reinterpret_cast<int64_t*>(smem);  // [R]
   float* Ws = smem + 2 * R;        // [64][ldk]
   float* Xs = Ws + H0 * ldk;       // [R][ldk]
   float* red = Xs + R * ldk;       // [128]
   float* shl = red + 2 * H0;       // [64] moment shift = Z0 of batch row 0
   float* x0 = shl + H0;            // [kp] X of batch row 0
+  float* part = x0 + kp;           // [4][64]
+  TT_STAMP(0, 0);
 
+  float bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias[j] = T.b0[16 * j + r];
   if (a.state && blockIdx.x == 0 && t == 0 && threadIdx.x == 0) a.state->step_cur = step;
   stage_ridx<R>(a, base, r0, ridx);
   if (threadIdx.x < 2 * H0) red[threadIdx.x] = 0.f;
@@ -208,53 +236,61 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
   }
   stage_w<NTH>(T.W0, H0, T.in_dim, kp, Ws, ldk);
   __syncthreads();
+  TT_STAMP(0, 1);
+  if (t == 0 && a.target && threadIdx.x < R) {  // (target, weight) of the tile's rows for k_top
+    const int64_t dr = ridx[threadIdx.x];
+    const float tv = a.target[dr], wv = a.weight[dr];
+    *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + threadIdx.x)) = make_float2(tv, wv);
+  }
   stage_x<R, NTH>(T, ridx, Xs, ldk);
   __syncthreads();
+  TT_STAMP(0, 2);
 
-  if (a.train && threadIdx.x < H0) {
+  if (a.train) {
     // Shifted moment sums: every block derives the same shift (Z0 of the
     // batch's first row, identical fp32 ops in every block), which keeps
     // var = S2/B - (S1/B)^2 free of cancellation for any data offset.
-    const int c = threadIdx.x;
-    float z = 0.f;
-    for (int k = 0; k < T.in_dim; ++k) z = fmaf(x0[k], Ws[c * ldk + k], z);
-    z += T.b0[c];
-    shl[c] = z;
-    if (blockIdx.x == 0) T.shift0[c] = z;
+    row_dot<NTH>(x0, Ws, ldk, T.in_dim, H0, T.b0, part, shl);
+    if (blockIdx.x == 0 && threadIdx.x < H0) T.shift0[threadIdx.x] = shl[threadIdx.x];
   }
-  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = zero4();
   strip_gemm_nt<4>(Xs + 16 * w * ldk, ldk, Ws, ldk, kp, acc);
   __syncthreads();
+  TT_STAMP(0, 3);
 
   float s1[4], s2[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = 16 * j + r;
-    const float bias = T.b0[col];
     const float sh = a.train ? shl[col] : 0.f;
     s1[j] = 0.f;
     s2[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t row = r0 + 16 * w + 4 * g + i;
-      const float z = acc[j][i] + bias;
-      if (row < a.B) {
-        T.Z0[row * H0 + col] = z;
-        const float d = z - sh;
-        s1[j] += d;
-        s2[j] += d * d;
-      }
+      const float z = acc[j][i] + bias[j];
+      acc[j][i] = z;
+      const float d = row < a.B ? z - sh : 0.f;
+      s1[j] += d;
+      s2[j] += d * d;
     }
   }
   if (a.train) {
     cols_to_lds<4>(s1, red);
     cols_to_lds<4>(s2, red + H0);
+  }
+  // Z0 (workspace rows are padded to whole tiles: no guard)
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) T.Z0[(r0 + 16 * w + 4 * g + i) * H0 + 16 * j + r] = acc[j][i];
+  if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H0) atomicAdd(&T.st0[threadIdx.x], red[threadIdx.x]);
   }
+  TT_STAMP(0, 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -263,7 +299,8 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
 template <int R>
 struct L4Lds {
   static constexpr int LD = H0 + 4;
-  static constexpr size_t bytes = sizeof(float) * ((size_t)(H1 + R) * LD + 3 * H0 + 2 * H1 + H0 + H1);
+  static constexpr size_t bytes =
+      sizeof(float) * ((size_t)(H1 + R) * LD + 3 * H0 + 2 * H1 + H0 + H1 + 4 * H1);
 };
 
 template <int R>
@@ -276,22 +313,27 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
   const TowerDev& T = a.tw[t];
   const int64_t step = step_current(a);
   const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   float* W4s = smem;               // [32][68]
   float* A0s = W4s + H1 * LD;      // [R][68]
   float* cf = A0s + R * LD;        // mean[64] alpha[64] beta[64]
   float* red = cf + 3 * H0;        // [64]
   float* a0r = red + 2 * H1;       // [64] A0 of batch row 0
   float* shl = a0r + H0;           // [32] moment shift = Z4 of batch row 0
+  float* part = shl + H1;          // [4][32]
+  TT_STAMP(1, 0);
 
-  // issue every load of the phase first
+  // issue every load of the phase first (Z0 rows are padded: no clamp needed)
   float4 z[Z4PT];
 #pragma unroll
   for (int k = 0; k < Z4PT; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int rl = e >> 4, c4 = (e & 15) * 4;
-    const int64_t row = min(r0 + rl, a.B - 1);
-    z[k] = *reinterpret_cast<const float4*>(T.Z0 + row * H0 + c4);
+    z[k] = *reinterpret_cast<const float4*>(T.Z0 + (r0 + rl) * H0 + c4);
   }
+  float bias[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bias[j] = T.b4[16 * j + r];
   const float z0r = threadIdx.x < H0 ? T.Z0[threadIdx.x] : 0.f;
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
@@ -305,6 +347,7 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
   if (threadIdx.x < 2 * H1) red[threadIdx.x] = 0.f;
   g2s_f4<NTH, 2>(T.W4, H0, W4s, LD, H1, H0);
   __syncthreads();
+  TT_STAMP(1, 1);
 
   const bool drop = a.train && a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
@@ -325,46 +368,47 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
     a0r[c] = bn_relu_drop(z0r, cf[c], cf[H0 + c], cf[2 * H0 + c], drop, key, (uint64_t)c, a.drop_thr, a.drop_scale);
   }
   __syncthreads();
+  TT_STAMP(1, 2);
 
-  if (a.train && threadIdx.x < H1) {  // shift for the BN1 moment sums (see k_l0_fwd)
-    const int c = threadIdx.x;
-    float zz = 0.f;
-    for (int k = 0; k < H0; ++k) zz = fmaf(a0r[k], W4s[c * LD + k], zz);
-    zz += T.b4[c];
-    shl[c] = zz;
-    if (blockIdx.x == 0) T.shift1[c] = zz;
+  if (a.train) {  // shift for the BN1 moment sums (see k_l0_fwd)
+    row_dot<NTH>(a0r, W4s, LD, H0, H1, T.b4, part, shl);
+    if (blockIdx.x == 0 && threadIdx.x < H1) T.shift1[threadIdx.x] = shl[threadIdx.x];
   }
-  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   f32x4 acc[2] = {zero4(), zero4()};
   strip_gemm_nt<2>(A0s + 16 * w * LD, LD, W4s, LD, H0, acc);
   __syncthreads();
+  TT_STAMP(1, 3);
 
   float s1[2], s2[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = 16 * j + r;
-    const float bias = T.b4[col];
     const float sh = a.train ? shl[col] : 0.f;
     s1[j] = 0.f;
     s2[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t row = r0 + 16 * w + 4 * g + i;
-      const float zz = acc[j][i] + bias;
-      if (row < a.B) {
-        T.Z4[row * H1 + col] = zz;
-        const float d = zz - sh;
-        s1[j] += d;
-        s2[j] += d * d;
-      }
+      const float zz = acc[j][i] + bias[j];
+      acc[j][i] = zz;
+      const float d = row < a.B ? zz - sh : 0.f;
+      s1[j] += d;
+      s2[j] += d * d;
     }
   }
   if (a.train) {
     cols_to_lds<2>(s1, red);
     cols_to_lds<2>(s2, red + H1);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) T.Z4[(r0 + 16 * w + 4 * g + i) * H1 + 16 * j + r] = acc[j][i];
+  if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H1) atomicAdd(&T.st1[threadIdx.x], red[threadIdx.x]);
   }
+  TT_STAMP(1, 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -374,7 +418,6 @@ template <int NDT, int R>
 struct TopLds {
   static constexpr int DP = 16 * NDT;
   static constexpr int LDA = H1 + 4;
-  static constexpr int LDD = DP + 4;
   static constexpr int W8s = 0;
   static constexpr int A1s = W8s + DP * LDA;
   static constexpr int Z4s = A1s + R * LDA;
@@ -385,8 +428,7 @@ struct TopLds {
   static constexpr int cf1 = db8 + DP;
   static constexpr int red = cf1 + 2 * 4 * H1;
   static constexpr int scal = red + 2 * H1;  // [0] loss part [1] dls part
-  static constexpr int ridx = scal + 4;      // int64 [R]
-  static constexpr int total = ridx + 2 * R;
+  static constexpr int total = scal + 4;
 };
 
 template <int NDT, int R>
@@ -400,24 +442,23 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   const int own = bwd ? (int)blockIdx.y : 0;
   const int oth = 1 - own;
   const int64_t step = step_current(a);
-  const int64_t base = batch_row0(a, step);
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   const int D = a.D;
-  int64_t* ridx = reinterpret_cast<int64_t*>(smem + L::ridx);
   float* W8s = smem + L::W8s;
   float* A1s = smem + L::A1s;
   float* Z4s = smem + L::Z4s;
+  TT_STAMP(2, 0);
 
-  // ---- phase 0: issue the loads of both towers' operands
+  // ---- phase 0: issue every load: both towers' Z4 tile and W8, biases,
+  // logit_scale, per-row (target, weight) or dscore
   float4 zo[ZPT], zs[ZPT], wo[WPT], ws[WPT];
 #pragma unroll
   for (int k = 0; k < ZPT; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int rl = e >> 3, c4 = (e & 7) * 4;
-    const int64_t row = min(r0 + rl, a.B - 1);
-    zo[k] = *reinterpret_cast<const float4*>(a.tw[oth].Z4 + row * H1 + c4);
-    zs[k] = *reinterpret_cast<const float4*>(a.tw[own].Z4 + row * H1 + c4);
+    zo[k] = *reinterpret_cast<const float4*>(a.tw[oth].Z4 + (r0 + rl) * H1 + c4);
+    zs[k] = *reinterpret_cast<const float4*>(a.tw[own].Z4 + (r0 + rl) * H1 + c4);
   }
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
@@ -425,19 +466,26 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     wo[k] = reinterpret_cast<const float4*>(a.tw[oth].W8)[e];
     ws[k] = reinterpret_cast<const float4*>(a.tw[own].W8)[e];
   }
-  // per-row target / weight (or dscore) of this lane's 4 rows
+  float bo[NDT], bs[NDT];
+#pragma unroll
+  for (int j = 0; j < NDT; ++j) {
+    const int d = min(16 * j + r, D - 1);
+    bo[j] = a.tw[oth].b8[d];
+    bs[j] = a.tw[own].b8[d];
+  }
+  const float lsc = *a.logit_scale;
   float tg[4], wt[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t row = min(r0 + 16 * w + 4 * g + i, a.B - 1);
+    const int64_t row = r0 + 16 * w + 4 * g + i;
     tg[i] = 0.f;
     wt[i] = 0.f;
     if (a.mode == TOP_TRAIN) {
-      const int64_t dr = data_row(a, base, row);
-      tg[i] = a.target[dr];
-      wt[i] = a.weight[dr];
+      const float2 v = *reinterpret_cast<const float2*>(a.tgw + 2 * row);
+      tg[i] = v.x;
+      wt[i] = v.y;
     } else if (a.mode == TOP_BWD_GIVEN) {
-      tg[i] = a.dscore[row];
+      tg[i] = a.dscore[min(row, a.B - 1)];
     }
   }
   if (threadIdx.x < 2 * H1) {
@@ -454,8 +502,8 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   }
   if (threadIdx.x < L::DP) smem[L::db8 + threadIdx.x] = 0.f;
   if (threadIdx.x < 2 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;  // red + scal
-  stage_ridx<R>(a, base, r0, ridx);
   __syncthreads();
+  TT_STAMP(2, 1);
 
   const bool drop = a.train && a.drop_thr > 0;
   // write one tower's A1 (and optionally raw Z4) + W8 into LDS
@@ -485,29 +533,28 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
       }
     }
   };
-  auto gemm = [&](int tau, f32x4(&acc)[NDT]) {
+  auto gemm = [&](const float(&bias)[NDT], f32x4(&acc)[NDT]) {
 #pragma unroll
     for (int j = 0; j < NDT; ++j) acc[j] = zero4();
     strip_gemm_nt<NDT>(A1s + 16 * w * L::LDA, L::LDA, W8s, L::LDA, H1, acc);
-    const TowerDev& T = a.tw[tau];
 #pragma unroll
-    for (int j = 0; j < NDT; ++j) {
-      const int d = 16 * j + r;
-      acc[j] += d < D ? T.b8[d] : 0.f;
-    }
+    for (int j = 0; j < NDT; ++j) acc[j] += (16 * j + r < D) ? bias[j] : 0.f;
   };
 
   f32x4 accO[NDT], accS[NDT];
   put(oth, zo, wo, false);
   __syncthreads();
-  gemm(oth, accO);
+  TT_STAMP(2, 2);
+  gemm(bo, accO);
   __syncthreads();
+  TT_STAMP(2, 3);
   put(own, zs, ws, bwd);
   __syncthreads();
-  gemm(own, accS);
+  TT_STAMP(2, 4);
+  gemm(bs, accS);
 
   // ---- cosine (symmetric in own/other: no runtime choice of register arrays)
-  const float s = expf(*a.logit_scale);
+  const float s = expf(lsc);
   float no[4], nt[4], cs[4], ds[4], sc[4];
   bool valid[4];
   float loss_p = 0.f, dls_p = 0.f;
@@ -529,17 +576,22 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     sc[i] = cs[i] * s;
     const int64_t row = r0 + 16 * w + 4 * g + i;
     valid[i] = row < a.B;
-    ds[i] = 0.f;
-    if (valid[i]) {
-      if (a.mode == TOP_TRAIN) {
-        const float diff = sc[i] - tg[i];
-        ds[i] = 2.f * diff * (wt[i] * (1.f / (float)a.B));
-        loss_p += wt[i] * diff * diff;
-      } else if (a.mode == TOP_BWD_GIVEN) {
-        ds[i] = tg[i];
-      }
-      dls_p += ds[i] * sc[i];
-      if (a.score && r == 0 && own == 0) a.score[row] = sc[i];
+    float dsi = 0.f;
+    if (a.mode == TOP_TRAIN) {
+      const float diff = sc[i] - tg[i];
+      dsi = 2.f * diff * (wt[i] * (1.f / (float)a.B));
+      loss_p += valid[i] ? wt[i] * diff * diff : 0.f;
+    } else if (a.mode == TOP_BWD_GIVEN) {
+      dsi = tg[i];
+    }
+    ds[i] = valid[i] ? dsi : 0.f;
+    dls_p += ds[i] * sc[i];
+  }
+  if (a.score && own == 0 && r == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = r0 + 16 * w + 4 * g + i;
+      if (row < a.B) a.score[row] = sc[i];
     }
   }
   if (!bwd) return;
@@ -591,20 +643,29 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     if (g == 0) atomicAdd(smem + L::db8 + 16 * j + r, cb);
   }
   __syncthreads();
+  TT_STAMP(2, 5);
 
   // dW8 = dU^T A1 over all R rows of the tile: each wave owns whole output
-  // tiles (no cross-wave reduction) and stores them into this tile's slab.
+  // tiles (no cross-wave reduction) and stores them into this tile's slab
+  // (rows d >= D of dU are zero: the padded slab rows are never read).
   float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
   for (int p = w; p < NDT; p += R / 16) {
     f32x4 acc[2] = {zero4(), zero4()};
     strip_gemm_nt<2>(dUT + 16 * p * L::LDT, L::LDT, A1T, L::LDT, R, acc);
+    if (16 * p + 16 <= D) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < 2; ++q)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int d = 16 * p + 4 * g + i;
-        if (d < D) slab[T.so_W8 + d * H1 + 16 * q + r] = acc[q][i];
-      }
+        for (int i = 0; i < 4; ++i) slab[T.so_W8 + (16 * p + 4 * g + i) * H1 + 16 * q + r] = acc[q][i];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int d = 16 * p + 4 * g + i;
+          if (d < D) slab[T.so_W8 + d * H1 + 16 * q + r] = acc[q][i];
+        }
+    }
   }
 
   // dA1 = dU W8  (A from the transposed dU image, W8s row-major [d][k])
@@ -622,18 +683,16 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     sb[q] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int64_t row = r0 + 16 * w + 4 * g + i;
-      const float dy = a1[q][i] > 0.f ? dA[q][i] * scl : 0.f;
-      if (row < a.B) {
-        T.dY1[row * H1 + col] = dy;
-        sg[q] += dy * ((z4[q][i] - mean) * inv);
-        sb[q] += dy;
-      }
+      const float dy = a1[q][i] > 0.f ? dA[q][i] * scl : 0.f;  // 0 on rows >= B (dU = 0)
+      T.dY1[(r0 + 16 * w + 4 * g + i) * H1 + col] = dy;
+      sg[q] += dy * ((z4[q][i] - mean) * inv);
+      sb[q] += dy;
     }
   }
   cols_to_lds<2>(sg, smem + L::red);
   cols_to_lds<2>(sb, smem + L::red + H1);
   __syncthreads();
+  TT_STAMP(2, 6);
 
   if (threadIdx.x < H1) {
     atomicAdd(&T.gg1[threadIdx.x], smem[L::red + threadIdx.x]);
@@ -643,7 +702,8 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     atomicAdd(a.g_ls, smem[L::scal + 1]);
     if (a.mode == TOP_TRAIN && a.loss_sum) atomicAdd(a.loss_sum, smem[L::scal + 0] / (float)a.B);
   }
-  for (int e = threadIdx.x; e < D; e += NTH) slab[T.so_b8 + e] = smem[L::db8 + e];
+  if (threadIdx.x < D) slab[T.so_b8 + threadIdx.x] = smem[L::db8 + threadIdx.x];
+  TT_STAMP(2, 7);
 }
 
 // ---------------------------------------------------------------------------
@@ -675,12 +735,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   float* c1 = db4 + H1;               // k1[32] mb[32] mg[32] mean1[32] inv1[32]
   float* c0 = c1 + 5 * H1;            // mean0[64] alpha0[64] beta0[64] inv0[64]
   float* red = c0 + 4 * H0;           // [128]
+  TT_STAMP(3, 0);
 
   // issue the phase's loads: dY1, Z4 (2 tiles), Z0 (4 tiles) in C layout
   f32x4 dy1[2], zz4[2], zz0[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t row = min(r0 + 16 * w + 4 * g + i, a.B - 1);
+    const int64_t row = r0 + 16 * w + 4 * g + i;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       dy1[q][i] = T.dY1[row * H1 + 16 * q + r];
@@ -710,6 +771,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   if (threadIdx.x < 2 * H0) red[threadIdx.x] = 0.f;
   g2s_f4<NTH, 2>(T.W4, H0, W4s, LDW, H1, H0);
   __syncthreads();
+  TT_STAMP(3, 1);
 
   // dZ4 (BN1 backward) and the recomputed A0 / normalised Z0, all C layout;
   // transposed images for the rows-contracted dW4 product
@@ -739,14 +801,15 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
       const int64_t row = r0 + 16 * w + 4 * g + i;
       const float z = zz0[j][i];
       const bool ok = row < a.B;
-      a0[j][i] = ok ? bn_relu_drop(z, c0[col], c0[H0 + col], c0[2 * H0 + col], drop, key, (uint64_t)row * H0 + col,
-                                   a.drop_thr, a.drop_scale)
-                    : 0.f;
+      const float av = bn_relu_drop(z, c0[col], c0[H0 + col], c0[2 * H0 + col], drop, key,
+                                    (uint64_t)row * H0 + col, a.drop_thr, a.drop_scale);
+      a0[j][i] = ok ? av : 0.f;
       zh0[j][i] = ok ? (z - c0[col]) * c0[3 * H0 + col] : 0.f;
     }
     store_tile_T(A0T, LDT, 16 * j, 16 * w, a0[j]);
   }
   __syncthreads();
+  TT_STAMP(3, 2);
 
   // dW4 = dZ4^T A0 over the tile's rows: wave w owns h1-tile (w&1) x h0-tiles
   // 2*(w>>1)..+1 and writes them straight into this tile's slab
@@ -773,23 +836,22 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     sb[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int64_t row = r0 + 16 * w + 4 * g + i;
-      const float dy = a0[j][i] > 0.f ? dA[j][i] * scl : 0.f;
-      if (row < a.B) {
-        T.dY0[row * H0 + col] = dy;
-        sg[j] += dy * zh0[j][i];
-        sb[j] += dy;
-      }
+      const float dy = a0[j][i] > 0.f ? dA[j][i] * scl : 0.f;  // 0 on rows >= B (a0 = 0)
+      T.dY0[(r0 + 16 * w + 4 * g + i) * H0 + col] = dy;
+      sg[j] += dy * zh0[j][i];
+      sb[j] += dy;
     }
   }
   cols_to_lds<4>(sg, red);
   cols_to_lds<4>(sb, red + H0);
   __syncthreads();
+  TT_STAMP(3, 3);
   if (threadIdx.x < H0) {
     atomicAdd(&T.gg0[threadIdx.x], red[threadIdx.x]);
     atomicAdd(&T.gbe0[threadIdx.x], red[H0 + threadIdx.x]);
   }
   if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = db4[threadIdx.x];
+  TT_STAMP(3, 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -827,11 +889,12 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   float* dZT = XT + FirstLds<R>::xt_floats(kp);        // [64][R+4]
   float* db0 = dZT + H0 * LDT;                         // [64]
   float* c0 = db0 + H0;                                // k0[64] mb[64] mg[64] mean0[64] inv0[64]
+  TT_STAMP(4, 0);
 
   f32x4 dy0[4], zz0[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t row = min(r0 + 16 * w + 4 * g + i, a.B - 1);
+    const int64_t row = r0 + 16 * w + 4 * g + i;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       dy0[j][i] = T.dY0[row * H0 + 16 * j + r];
@@ -851,29 +914,49 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     db0[c] = 0.f;
   }
   __syncthreads();
+  TT_STAMP(4, 1);
 
   // X^T tile: consecutive threads take consecutive rows (conflict-free LDS
   // writes); gathered 16-B row loads, all issued before the stores
   if (T.num_vec) {
     const int c4n = T.n_num >> 2, n4 = R * c4n;
     constexpr int UNR = 4;
-    for (int b0 = 0; b0 < n4; b0 += NTH * UNR) {
-      float4 v[UNR];
+    if (n4 % (NTH * UNR) == 0) {
+      for (int b0 = 0; b0 < n4; b0 += NTH * UNR) {
+        float4 v[UNR];
 #pragma unroll
-      for (int k = 0; k < UNR; ++k) {
-        const int e = min(b0 + (int)threadIdx.x + k * NTH, n4 - 1);
-        const int rr = e % R, c4 = e / R;
-        v[k] = *reinterpret_cast<const float4*>(T.num + ridx[rr] * T.num_ld + 4 * c4);
-      }
+        for (int k = 0; k < UNR; ++k) {
+          const int e = b0 + (int)threadIdx.x + k * NTH;
+          v[k] = *reinterpret_cast<const float4*>(T.num + ridx[e % R] * T.num_ld + 4 * (e / R));
+        }
 #pragma unroll
-      for (int k = 0; k < UNR; ++k) {
-        const int e = b0 + (int)threadIdx.x + k * NTH;
-        if (e < n4) {
+        for (int k = 0; k < UNR; ++k) {
+          const int e = b0 + (int)threadIdx.x + k * NTH;
           const int rr = e % R, c = 4 * (e / R);
           XT[(c + 0) * LDT + rr] = v[k].x;
           XT[(c + 1) * LDT + rr] = v[k].y;
           XT[(c + 2) * LDT + rr] = v[k].z;
           XT[(c + 3) * LDT + rr] = v[k].w;
+        }
+      }
+    } else {
+      for (int b0 = 0; b0 < n4; b0 += NTH * UNR) {
+        float4 v[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+          const int e = min(b0 + (int)threadIdx.x + k * NTH, n4 - 1);
+          v[k] = *reinterpret_cast<const float4*>(T.num + ridx[e % R] * T.num_ld + 4 * (e / R));
+        }
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+          const int e = b0 + (int)threadIdx.x + k * NTH;
+          if (e < n4) {
+            const int rr = e % R, c = 4 * (e / R);
+            XT[(c + 0) * LDT + rr] = v[k].x;
+            XT[(c + 1) * LDT + rr] = v[k].y;
+            XT[(c + 2) * LDT + rr] = v[k].z;
+            XT[(c + 3) * LDT + rr] = v[k].w;
+          }
         }
       }
     }
@@ -913,6 +996,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     if (g == 0) atomicAdd(db0 + col, cb);
   }
   __syncthreads();
+  TT_STAMP(4, 2);
 
   // dW0 = dZ0^T X over the tile's rows: wave w owns outputs 16w..16w+15 and
   // every input column tile; results go straight into this tile's slab
@@ -920,9 +1004,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   const int in = T.in_dim;
   auto put_w0 = [&](int kt, const f32x4& acc) {
     const int k = 16 * kt + r;
-    if (k < in) {
+    float* dst = slab + T.so_W0 + (16 * w + 4 * g) * in + k;
+    if (16 * kt + 16 <= in) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) slab[T.so_W0 + (16 * w + 4 * g + i) * in + k] = acc[i];
+      for (int i = 0; i < 4; ++i) dst[i * in] = acc[i];
+    } else if (k < in) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[i * in] = acc[i];
     }
   };
   int kt = 0;
@@ -963,6 +1051,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     }
   }
   if (threadIdx.x < H0) slab[T.so_b0 + threadIdx.x] = db0[threadIdx.x];
+  TT_STAMP(4, 3);
 }
 
 template __global__ void k_l0_fwd<64>(StepArgs);

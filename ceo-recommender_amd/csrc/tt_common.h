@@ -97,20 +97,45 @@ __device__ __forceinline__ void cl_gemm_tn(const f32x4& P, const f32x4& Q, f32x4
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// sum over the 4 lane groups (g = l>>4) that share a column r
-__device__ __forceinline__ float col_reduce(float v) {
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+// Cross-lane sums without LDS round trips (ds_bpermute costs a full LDS
+// latency per step and the compiler serialises dependent ones):
+//  * within a 16-lane row: DPP quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+//    row_mirror -- each step pairs disjoint partial sums, so after four steps
+//    every lane of the row holds the same total;
+//  * across rows: gfx950 v_permlane16_swap / v_permlane32_swap exchange whole
+//    rows between two registers in one VALU op.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+__device__ __forceinline__ float xrow16_add(float v) {  // v[l] + v[l ^ 16]
+  const unsigned u = __float_as_uint(v);
+  const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  // copy the elements out first: __builtin_bit_cast(float, p[1]) is folded
+  // into p[0] by this hipcc
+  const unsigned lo = p[0], hi = p[1];
+  return __uint_as_float(lo) + __uint_as_float(hi);
+}
+__device__ __forceinline__ float xrow32_add(float v) {  // v[l] + v[l ^ 32]
+  const unsigned u = __float_as_uint(v);
+  const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  // copy the elements out first: __builtin_bit_cast(float, p[1]) is folded
+  // into p[0] by this hipcc
+  const unsigned lo = p[0], hi = p[1];
+  return __uint_as_float(lo) + __uint_as_float(hi);
+}
+// sum over the 4 lane groups (g = l>>4) that share a column r
+__device__ __forceinline__ float col_reduce(float v) { return xrow32_add(xrow16_add(v)); }
 // sum over the 16 lanes (r) that share a row group g
 __device__ __forceinline__ float row_reduce16(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
   return v;
 }
+// full-wave sum (every lane gets the total)
+__device__ __forceinline__ float wave_reduce(float v) { return col_reduce(row_reduce16(v)); }
 
 // ---------------------------------------------------------------------------
 // Counter-based dropout RNG (restated in oracle/two_tower.py dropout_keep_mask)

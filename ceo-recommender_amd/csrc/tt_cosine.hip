@@ -6,7 +6,7 @@
 // reverse (SURVEY.md 3D closed form).
 //
 // HBM-bound streaming kernel: one row per 16-lane group (4 rows per wave in
-// flight), 16-byte loads/stores, row reductions with wave shuffles, each
+// flight), 16-byte loads/stores, row reductions with DPP, each
 // row's u and v kept in registers between the reduction and the gradient
 // (read once, written once: 4(4D+3) bytes per pair for fwd+bwd).  Loss and
 // logit-scale partials are reduced per block and added with one atomic each.
@@ -90,10 +90,8 @@ __global__ __launch_bounds__(COS_THREADS) void k_cosine(const float* __restrict_
     }
   }
   if (BWD) {
-    for (int o = 32; o > 0; o >>= 1) {
-      loss_p += __shfl_xor(loss_p, o);
-      dls_p += __shfl_xor(dls_p, o);
-    }
+    loss_p = wave_reduce(loss_p);
+    dls_p = wave_reduce(dls_p);
     if (l == 0) {
       red[0][wave_id()] = loss_p;
       red[1][wave_id()] = dls_p;
@@ -152,10 +150,8 @@ __global__ __launch_bounds__(COS_THREADS) void k_cosine_scalar(const float* __re
     }
   }
   if (BWD) {
-    for (int o = 32; o > 0; o >>= 1) {
-      loss_p += __shfl_xor(loss_p, o);
-      dls_p += __shfl_xor(dls_p, o);
-    }
+    loss_p = wave_reduce(loss_p);
+    dls_p = wave_reduce(dls_p);
     if (lane_id() == 0) {
       atomicAdd(loss_sum, loss_p * inv_batch);
       atomicAdd(dls_sum, dls_p);

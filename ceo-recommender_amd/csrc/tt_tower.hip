@@ -555,9 +555,10 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
 
   // ---- cosine (symmetric in own/other: no runtime choice of register arrays)
   const float s = expf(lsc);
-  float no[4], nt[4], cs[4], ds[4], sc[4];
+  float ino[4], int_[4], cs[4], ds[4], sc[4];
   bool valid[4];
   float loss_p = 0.f, dls_p = 0.f;
+  const float inv_b = 1.f / (float)a.B;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float uv = 0.f, oo = 0.f, tt2 = 0.f;
@@ -570,16 +571,16 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     uv = row_reduce16(uv);
     oo = row_reduce16(oo);
     tt2 = row_reduce16(tt2);
-    no[i] = sqrtf(oo);
-    nt[i] = sqrtf(tt2);
-    cs[i] = uv / (no[i] * nt[i]);
+    ino[i] = __builtin_amdgcn_rsqf(oo);  // v_rsq_f32 (1 ulp): no IEEE divides
+    int_[i] = __builtin_amdgcn_rsqf(tt2);
+    cs[i] = uv * ino[i] * int_[i];
     sc[i] = cs[i] * s;
     const int64_t row = r0 + 16 * w + 4 * g + i;
     valid[i] = row < a.B;
     float dsi = 0.f;
     if (a.mode == TOP_TRAIN) {
       const float diff = sc[i] - tg[i];
-      dsi = 2.f * diff * (wt[i] * (1.f / (float)a.B));
+      dsi = 2.f * diff * (wt[i] * inv_b);
       loss_p += valid[i] ? wt[i] * diff * diff : 0.f;
     } else if (a.mode == TOP_BWD_GIVEN) {
       dsi = tg[i];
@@ -597,11 +598,8 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   if (!bwd) return;
 
   if (own == 0) {  // loss + logit_scale grad once per row tile
-    float lp = (r == 0) ? loss_p : 0.f, dp = (r == 0) ? dls_p : 0.f;
-    for (int o = 32; o > 0; o >>= 1) {
-      lp += __shfl_xor(lp, o);
-      dp += __shfl_xor(dp, o);
-    }
+    // every lane of a row group holds the same loss_p / dls_p: sum over g
+    const float lp = col_reduce(loss_p), dp = col_reduce(dls_p);
     if (l == 0) {
       atomicAdd(smem + L::scal + 0, lp);
       atomicAdd(smem + L::scal + 1, dp);
@@ -614,9 +612,8 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float dc = ds[i] * s;
-    const float ino = 1.f / no[i], int_ = 1.f / nt[i];
-    const float ka = valid[i] ? dc * ino * int_ : 0.f;
-    const float kb = valid[i] ? dc * cs[i] * ino * ino : 0.f;
+    const float ka = valid[i] ? dc * ino[i] * int_[i] : 0.f;
+    const float kb = valid[i] ? dc * cs[i] * ino[i] * ino[i] : 0.f;
 #pragma unroll
     for (int j = 0; j < NDT; ++j) dO[j][i] = ka * accO[j][i] - kb * accS[j][i];
   }

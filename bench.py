@@ -153,9 +153,24 @@ def cosine_roofline(dev, D=128, n=1 << 22, reps=20):
     ms = e0.elapsed_time(e1) / reps
     byts = 4 * (4 * D + 3) * n
     gbs = byts / (ms * 1e-3) / 1e9
+    # measured stream peak on the same box: device copy of a 2 GiB buffer
+    # (read + write bytes / time), the practical HBM ceiling next to the spec
+    src = torch.empty(1 << 29, device=dev)
+    dst = torch.empty_like(src)
+    for _ in range(2):
+        dst.copy_(src)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(10):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    stream = 2 * src.numel() * 4 / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9
+    del src, dst
     return {"kernel": "k_cosine<2,true>", "pairs": n, "D": D, "bytes_per_pair": 4 * (4 * D + 3),
             "avg_us": round(ms * 1e3, 2), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(gbs / PEAK_HBM_GBS, 4), "pairs_per_s": round(n / (ms * 1e-3), 1)}
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "stream_peak_measured": round(stream, 1),
+            "frac_of_measured_stream": round(gbs / stream, 4), "pairs_per_s": round(n / (ms * 1e-3), 1)}
 
 
 def main():

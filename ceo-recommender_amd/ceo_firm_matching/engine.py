@@ -19,6 +19,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _native as N
+from .distributed import average_gradients_, broadcast_state_, world_of
 from .model import CEOFirmMatcher
 
 DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")
@@ -44,7 +45,9 @@ class FusedTrainer:
         self.hp = N.adam_hp(lr, betas, eps)
         self.seed = (int(torch.cuda.initial_seed()) if seed is None else int(seed)) & ((1 << 63) - 1)
         self.pg = process_group
-        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.world = world_of(process_group) if process_group is not None else 1
+        if self.world > 1:  # DDP construction semantics: rank 0's state everywhere
+            broadcast_state_(self.arena.params, self.arena.buffers, process_group)
         self.max_batch = 0
         self.ws = None
         self.ensure_batch(max_batch)
@@ -122,8 +125,7 @@ class FusedTrainer:
         self.steps_host += 1
 
     def allreduce_and_adam(self):
-        torch.distributed.all_reduce(self.grad, op=torch.distributed.ReduceOp.SUM, group=self.pg)
-        self.grad.mul_(1.0 / self.world)
+        average_gradients_(self.grad, self.pg)
         a = self.arena
         rc = self.lib.tt_adam_apply(a.params.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
                                     self.exp_avg_sq.data_ptr(), a.params.numel(), self.hp,

@@ -100,17 +100,16 @@ struct WsLayout {
 // beyond B unconditionally into this padding instead of branching per row).
 static int64_t padded_rows(int64_t b) { return round_up(std::max<int64_t>(b, 1), TOP_ROWS_MAX); }
 
+// Layout: the accumulators a fused step leaves zeroed for the next one (BN
+// moment sums, the atomic gradient arena) come first, at offsets that do not
+// depend on the batch size -- consecutive steps of different B (the last
+// partial batch of an epoch) must find them where the previous step zeroed
+// them.  Per-row arrays and per-tile partial slabs follow.
 static WsLayout make_ws(const Layout& L, int64_t max_batch) {
   WsLayout W;
   int64_t off = 0;
   auto take = [&](int64_t n) { const int64_t o = off; off += round_up(n, 64); return o; };
-  const int64_t rows = padded_rows(max_batch);
-  W.n_tiles = (int)(rows / ROWS);
   for (int t = 0; t < 2; ++t) {
-    W.Z0[t] = take(rows * H0);
-    W.Z4[t] = take(rows * H1);
-    W.dY0[t] = take(rows * H0);
-    W.dY1[t] = take(rows * H1);
     W.st0[t] = take(2 * H0);
     W.st1[t] = take(2 * H1);
     W.sh0[t] = take(H0);
@@ -118,9 +117,17 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
     W.fin0[t] = take(2 * H0);
     W.fin1[t] = take(2 * H1);
   }
+  W.gacc = take(L.n);
+  const int64_t rows = padded_rows(max_batch);
+  W.n_tiles = (int)(rows / ROWS);
+  for (int t = 0; t < 2; ++t) {
+    W.Z0[t] = take(rows * H0);
+    W.Z4[t] = take(rows * H1);
+    W.dY0[t] = take(rows * H0);
+    W.dY1[t] = take(rows * H1);
+  }
   W.tgw = take(rows * 2);
   for (int t = 0; t < 2; ++t) W.slab[t] = take((int64_t)W.n_tiles * L.slab_ld);
-  W.gacc = take(L.n);
   W.total = off;
   return W;
 }
@@ -319,8 +326,10 @@ struct Ctx {
   Plan P;
 };
 
-static int prepare(const tt_model_desc* d, const tt_batch* b, int64_t ws_bytes, Ctx* c) {
+// Every argument error is decided here, on the host, before any HIP call.
+static int prepare(const tt_model_desc* d, const tt_batch* b, int64_t ws_bytes, int64_t min_rows, Ctx* c) {
   if (!desc_ok(d) || !batch_ok(d, b)) return TT_ERR_ARG;
+  if (b->n_rows < min_rows) return TT_ERR_BATCH_TOO_SMALL;
   c->L = make_layout(d);
   int rc = make_plan(d, c->L, std::max<int64_t>(b->n_rows, 1), &c->P);
   if (rc) return rc;
@@ -394,9 +403,8 @@ int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, 
                    tt_stream_t stream) {
   if (!params || !buffers || !nbt || !ws || !score) return TT_ERR_ARG;
   Ctx c;
-  int rc = prepare(d, b, ws_bytes, &c);
+  int rc = prepare(d, b, ws_bytes, train ? 2 : 0, &c);
   if (rc) return rc;
-  if (train && b->n_rows < 2) return TT_ERR_BATCH_TOO_SMALL;
   if (b->n_rows == 0) return TT_OK;
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
@@ -424,9 +432,8 @@ int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch*
                     uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream) {
   if (!params || !dscore || !ws || !grad) return TT_ERR_ARG;
   Ctx c;
-  int rc = prepare(d, b, ws_bytes, &c);
+  int rc = prepare(d, b, ws_bytes, 2, &c);
   if (rc) return rc;
-  if (b->n_rows < 2) return TT_ERR_BATCH_TOO_SMALL;
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   // running-stat buffers are not touched by backward; pass a dummy-safe pointer
@@ -456,9 +463,8 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   if (apply_adam && (!hp || !exp_avg || !exp_avg_sq)) return TT_ERR_ARG;
   if (b && b->cycle > 0 && b->n_rows < 1) return TT_ERR_ARG;
   Ctx c;
-  int rc = prepare(d, b, ws_bytes, &c);
+  int rc = prepare(d, b, ws_bytes, 2, &c);
   if (rc) return rc;
-  if (b->n_rows < 2) return TT_ERR_BATCH_TOO_SMALL;
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   StepArgs a;

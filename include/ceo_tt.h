@@ -108,7 +108,10 @@ int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out /* TT_NUM_OFFSETS 
  * running_mean1[32] running_var1[32]; num_batches_tracked lives in a separate
  * int64[4] array (firm bn1, firm bn5, ceo bn1, ceo bn5). */
 int64_t tt_buffer_count(const tt_model_desc* d);
-/* Bytes of the zero-initialised workspace for batches of up to max_batch. */
+/* Bytes of the workspace for batches of up to max_batch.  Zero it once and
+ * keep it with its trainer: its leading region (offsets independent of the
+ * batch size) holds accumulators every fused step leaves zeroed for the next
+ * one, so steps of different B may share it.                                */
 int64_t tt_workspace_bytes(const tt_model_desc* d, int64_t max_batch);
 
 /* Forward of CEOFirmMatcher (model.py:67-89).  train=1: batch-statistics

@@ -1,0 +1,173 @@
+"""Host-side checks of the C-ABI boundary (no GPU needed).
+
+* libceo_tt.so loads and exports every entry point include/ceo_tt.h declares;
+* the ABI version and the constants of the header match the ctypes mirror;
+* the parameter arena layout (tt_param_offsets) is the module's parameter
+  set, 16-byte aligned and non-overlapping, for the golden geometries;
+* argument errors are reported on the host before anything is enqueued
+  (null pointers, unsupported shapes, short workspace, train-mode B < 2 ->
+  the same ValueError text as torch's BatchNorm).
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_golden, meta_of
+from ceo_firm_matching import CEOFirmMatcher, Config
+from ceo_firm_matching import _native as N
+
+HEADER = os.path.join(ROOT, "include", "ceo_tt.h")
+
+
+def header_text():
+    with open(HEADER) as f:
+        return f.read()
+
+
+def header_functions():
+    txt = re.sub(r"/\*.*?\*/", "", header_text(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|void)\s+(tt_\w+)\s*\(", txt, flags=re.M)))
+
+
+def header_define(name):
+    m = re.search(rf"#define\s+{name}\s+\(?(-?\d+)\)?", header_text())
+    assert m, name
+    return int(m.group(1))
+
+
+def test_library_exports_every_header_symbol():
+    L = N.lib()
+    names = header_functions()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(L, n), f"libceo_tt.so does not export {n}"
+    assert set(N.EXPORTED) <= set(names)
+
+
+def test_header_constants_match_binding():
+    assert N.lib().tt_abi_version() == header_define("TT_ABI_VERSION") == N.TT_ABI_VERSION
+    assert header_define("TT_MAX_CAT") == N.TT_MAX_CAT
+    for k in ("TT_OK", "TT_ERR_ARG", "TT_ERR_BATCH_TOO_SMALL", "TT_ERR_UNSUPPORTED", "TT_ERR_WORKSPACE"):
+        assert header_define(k) == getattr(N, k), k
+
+
+def test_struct_sizes_match_header_layout():
+    # tt_model_desc: 7 int32 + 32 int32 + 3 floats; tt_batch: 11 8-byte fields
+    assert ctypes.sizeof(N.TTModelDesc) == 4 * (7 + 2 * N.TT_MAX_CAT + 3)
+    assert ctypes.sizeof(N.TTBatch) == 8 * 15
+    assert ctypes.sizeof(N.TTAdamHP) == 16
+
+
+def _model(case):
+    g = load_golden(case)
+    cfg = Config()
+    cfg.LATENT_DIM = int(g["meta/latent"])
+    cfg.DEVICE = torch.device("cpu")
+    torch.manual_seed(0)
+    return CEOFirmMatcher(meta_of(g), cfg)
+
+
+@pytest.mark.parametrize("case", ["meta_test", "cfg2", "cfg3"])
+def test_param_arena_layout(case):
+    m = _model(case)
+    desc = m.tt_desc()
+    n = N.param_count(desc)
+    offs = N.param_offsets(desc)
+    slots = m._named_slots(offs)
+    names = [s[0] for s in slots]
+    assert sorted(names) == sorted(k for k, _ in m.named_parameters())
+    spans = sorted((off, off + p.numel(), name) for name, p, off in slots)
+    for (a0, a1, na), (b0, b1, nb) in zip(spans, spans[1:]):
+        assert a1 <= b0, f"{na} overlaps {nb}"
+    assert all(off % 4 == 0 for off, _, _ in spans), "parameters must start 16-byte aligned"
+    assert spans[-1][1] <= n < spans[-1][1] + 4 * len(spans)
+    # the arena binding keeps every value and is seen through state_dict
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    arena = m.bind_arena()
+    assert arena.params.numel() == n
+    after = m.state_dict()
+    assert before.keys() == after.keys()
+    for k in before:
+        assert torch.equal(before[k], after[k]), k
+    for name, p, off in m._named_slots(offs):
+        assert p.data_ptr() == arena.params.data_ptr() + 4 * off, name
+    assert N.lib().tt_buffer_count(ctypes.byref(desc)) == arena.buffers.numel()
+
+
+def test_workspace_bytes_grow_with_batch():
+    desc = _model("cfg3").tt_desc()
+    w = [N.workspace_bytes(desc, b) for b in (1, 128, 4096, 16384, 65536)]
+    assert all(x > 0 and x % 256 == 0 for x in w)
+    assert w == sorted(w) and w[-1] > w[0]
+    with pytest.raises(ValueError):
+        N.workspace_bytes(desc, 0)
+
+
+def _fake(n=1 << 20):
+    """A host buffer standing in for device pointers: argument errors are
+    decided before anything dereferences or enqueues."""
+    return np.zeros(n, dtype=np.float32)
+
+
+def _batch(desc, n_rows):
+    buf = _fake()
+    b = N.TTBatch()
+    for t in range(2):
+        b.num[t] = buf.ctypes.data
+        b.num_ld[t] = desc.n_num[t]
+        if desc.n_cat[t]:
+            b.cat[t] = buf.ctypes.data
+            b.cat_ld[t] = desc.n_cat[t]
+    b.target = buf.ctypes.data
+    b.weight = buf.ctypes.data
+    b.n_rows = n_rows
+    return b, buf
+
+
+def test_host_argument_errors():
+    L = N.lib()
+    m = _model("meta_test")
+    desc = m.tt_desc()
+    b, keep = _batch(desc, 64)
+    pbuf = _fake()
+    p = pbuf.ctypes.data
+    ws_ok = N.workspace_bytes(desc, 64)
+    fwd = lambda d, bb, train, ws_bytes, params=p: L.tt_forward(  # noqa: E731
+        ctypes.byref(d), params, p, p, ctypes.byref(bb), train, 0, 1, p, ws_bytes, p, None)
+    # null parameter pointer
+    assert fwd(desc, b, 0, ws_ok, params=None) == N.TT_ERR_ARG
+    # workspace too small
+    assert fwd(desc, b, 0, ws_ok - 4) == N.TT_ERR_WORKSPACE
+    # train-mode batch of one row (BatchNorm), both for forward and the fused step
+    b1, keep1 = _batch(desc, 1)
+    assert fwd(desc, b1, 1, ws_ok) == N.TT_ERR_BATCH_TOO_SMALL
+    hp = N.adam_hp(4e-4)
+    rc = L.tt_train_step(ctypes.byref(desc), p, p, p, ctypes.byref(b1), ctypes.byref(hp), 0, p, p, ws_ok,
+                         p, p, p, 1, None)
+    assert rc == N.TT_ERR_BATCH_TOO_SMALL
+    with pytest.raises(ValueError, match="Expected more than 1 value per channel when training"):
+        N.check(rc, "tt_train_step", 1, 64)
+    # unsupported geometry: LATENT_DIM beyond the fused top kernel
+    big = N.make_desc(desc.n_num, [[], []], desc.emb_dim, 512)
+    bb, keep2 = _batch(big, 64)
+    assert fwd(big, bb, 0, 1 << 40) == N.TT_ERR_UNSUPPORTED
+    # invalid descriptor (dropout p = 1, more categorical columns than supported)
+    bad = N.make_desc(desc.n_num, [[], []], desc.emb_dim, 64, dropout_p=1.0)
+    assert L.tt_param_count(ctypes.byref(bad)) == N.TT_ERR_ARG
+    with pytest.raises(NotImplementedError):
+        N.make_desc((1, 1), [[2] * 17, []], (4, 4), 8)
+    # cosine kernels: null pointers
+    assert L.tt_cosine_forward(None, p, 8, 16, p, p, None) == N.TT_ERR_ARG
+    assert L.tt_adam_apply(p, p, p, p, 10, ctypes.byref(hp), None, 0, None) == N.TT_ERR_ARG
+
+
+def test_product_path_refuses_without_extension(monkeypatch):
+    """A missing extension fails loudly (no CPU fallback on a HIP device)."""
+    monkeypatch.setattr(N, "_LIB", None)
+    monkeypatch.setattr(N, "LIB_PATH", os.path.join(ROOT, "does-not-exist", "libceo_tt.so"))
+    with pytest.raises(N.NativeLibraryError, match="HIP extension not built"):
+        N.lib()

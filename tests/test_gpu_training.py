@@ -1,0 +1,136 @@
+"""End-to-end drop-in checks on the GPU (through libceo_tt.so):
+
+* ``train_model`` on the HIP device runs the reference CLI pipeline
+  (cli.py:29-59, EPOCHS 6, dropout p = 0, torch.manual_seed(1234)) on the
+  fused engine and prints the reference's epoch lines; the final state_dict
+  matches the reference's (tests/golden/cli.npz);
+* data-parallel step: 2 ranks (processes) on the one GPU, gloo for the
+  collective, each rank one local-BN shard -> fused gradient, all-reduce
+  average, tt_adam_apply; parameters equal the reference's DDP step
+  (tests/golden/ddp.npz, G = 2).
+"""
+import contextlib
+import io
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import excluded_param, load_golden, meta_of, normwise, sub
+
+pytestmark = pytest.mark.gpu
+
+# 24 Adam steps amplify fp32 summation-order differences in grads that are
+# ~0 (Adam normalises them to +-lr steps); the 1e-5 bar holds per step
+# (test_gpu_parity); after 24 steps we allow 1e-4 normwise.
+TOL_TRAINED = 1e-4
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def test_train_model_cli_pipeline_on_fused_engine():
+    _need_gpu()
+    from torch.utils.data import DataLoader
+    from ceo_firm_matching import Config
+    from ceo_firm_matching.data import CEOFirmDataset
+    from ceo_firm_matching.training import train_model
+    from test_host_pipeline import cli_data
+    g = load_golden("cli")
+    cfg = Config()
+    cfg.EPOCHS = 6
+    cfg.DROPOUT_P = 0.0
+    cfg.DEVICE = torch.device("cuda")
+    train, val = cli_data(cfg)
+    torch.manual_seed(1234)
+    tl = DataLoader(CEOFirmDataset(train), batch_size=256, shuffle=True)
+    vl = DataLoader(CEOFirmDataset(val), batch_size=256, shuffle=False)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        model = train_model(tl, vl, train, cfg)
+    lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("Epoch")]
+    assert lines == list(g["printed"])
+    assert model._trainer.steps_done() == 6 * 4
+    sd = model.state_dict()
+    worst = {}
+    for k, ref in ((k[len("final/"):], v) for k, v in g.items() if k.startswith("final/")):
+        if excluded_param(k):
+            continue
+        got = sd[k].detach().cpu().numpy()
+        if got.dtype.kind == "i":
+            assert np.array_equal(got, ref), k
+        elif k.endswith("running_mean"):
+            # the running mean of Z = XW^T + b carries the pre-BN bias b, whose
+            # true gradient is 0 and whose fp32 noise Adam turns into +-lr steps
+            # (SURVEY 8c exclusion): bound the drift by steps * lr, absolute.
+            assert np.max(np.abs(got - ref)) <= 24 * cfg.LEARNING_RATE, k
+        else:
+            worst[k] = normwise(got, ref)
+    bad = {k: v for k, v in worst.items() if v >= TOL_TRAINED}
+    assert not bad, bad
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ddp_rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching import CEOFirmMatcher, Config
+        from ceo_firm_matching.engine import FusedTrainer
+        dev = torch.device("cuda:0")
+        g = load_golden("ddp")
+        meta = meta_of(load_golden("cfg2"))
+        cfg = Config()
+        cfg.LATENT_DIM = 64
+        cfg.DROPOUT_P = 0.0
+        cfg.DEVICE = dev
+        m = CEOFirmMatcher(meta, cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()})
+        m = m.to(dev)
+        if rank == 1:  # the broadcast must restore rank 0's weights
+            with torch.no_grad():
+                m.firm_tower[0].weight.add_(1.0)
+        tr = FusedTrainer(m, lr=cfg.LEARNING_RATE, max_batch=64, seed=0, process_group=dist.group.WORLD)
+        shard = {k: torch.from_numpy(v) for k, v in sub(g, f"G{world}/shard{rank}").items()}
+        tr.set_data(shard)
+        tr.step(None, 0, shard["target"].shape[0])
+        torch.cuda.synchronize()
+        ref = sub(g, f"G{world}/after_step")
+        errs = {}
+        for k, p in m.named_parameters():
+            if not excluded_param(k):
+                errs[k] = normwise(p.detach().cpu().numpy(), ref[k])
+        q.put((rank, max(errs.values()), max(errs, key=errs.get)))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, float("inf"), repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_step_two_ranks_one_gpu():
+    _need_gpu()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ddp_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=120)
+    for rank, err, where in res:
+        assert err < 1e-5, (rank, err, where)
+    assert all(p.exitcode == 0 for p in ps)

@@ -1,0 +1,117 @@
+"""Host-side plumbing of the drop-in (CPU, no GPU): the reference CLI
+pipeline (cli.py:29-59) pinned by tests/golden/cli.npz.
+
+* DataProcessor + split + fit/transform reproduce the reference's tensors
+  bit for bit (data.py:89-146, vectorised here);
+* ``sampler_batches`` yields exactly the DataLoader's batch order and leaves
+  the global RNG where ``iter(loader)`` leaves it (training.py:36-40);
+* ``train_model`` on CPU reproduces the reference's printed epoch lines and
+  final state_dict (EPOCHS 6, dropout p = 0, torch.manual_seed(1234));
+* ``python -m ceo_firm_matching.cli --synthetic`` runs end to end.
+"""
+import contextlib
+import io
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+from sklearn.model_selection import train_test_split
+from torch.utils.data import DataLoader
+
+from conftest import PKG_PARENT, excluded_param, load_golden, normwise
+from ceo_firm_matching import Config
+from ceo_firm_matching.data import CEOFirmDataset, DataProcessor
+from ceo_firm_matching.synthetic import generate_synthetic_data
+from ceo_firm_matching.training import sampler_batches, train_model
+
+KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")
+
+
+def cli_data(cfg):
+    proc = DataProcessor(cfg)
+    with contextlib.redirect_stdout(io.StringIO()):
+        df = proc.prepare_features(generate_synthetic_data(1000))
+        tr, va = train_test_split(df, test_size=0.2, random_state=42)
+        proc.fit(tr)
+        return proc.transform(tr), proc.transform(va)
+
+
+def test_processor_matches_reference_tensors():
+    g = load_golden("cli")
+    cfg = Config()
+    train, val = cli_data(cfg)
+    for k in KEYS:
+        np.testing.assert_array_equal(train[k].numpy(), g[f"train/{k}"], err_msg=k)
+        np.testing.assert_array_equal(val[k].numpy(), g[f"val/{k}"], err_msg=k)
+    assert list(train["firm_cat_counts"]) == list(g["meta/firm_cat_counts"])
+    assert list(train["ceo_cat_counts"]) == list(g["meta/ceo_cat_counts"])
+    assert train["n_firm_numeric"] == int(g["meta/n_firm_numeric"])
+    assert train["n_ceo_numeric"] == int(g["meta/n_ceo_numeric"])
+
+
+class _Idx(torch.utils.data.Dataset):
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return i
+
+
+@pytest.mark.parametrize("n,bs", [(800, 256), (1000, 128), (37, 64), (4096, 4096)])
+def test_sampler_batches_equal_dataloader_order(n, bs):
+    loader = DataLoader(_Idx(n), batch_size=bs, shuffle=True)
+    torch.manual_seed(7)
+    ours = [sampler_batches(loader) for _ in range(3)]
+    after_ours = torch.rand(4)
+    torch.manual_seed(7)
+    theirs = [[b.tolist() for b in loader] for _ in range(3)]
+    after_theirs = torch.rand(4)
+    assert ours == theirs
+    assert torch.equal(after_ours, after_theirs)
+    assert [len(b) for b in ours[0]][-1] == (n % bs or bs)  # last partial batch kept
+
+
+def test_train_model_cpu_matches_reference_cli_run():
+    g = load_golden("cli")
+    cfg = Config()
+    cfg.EPOCHS = 6
+    cfg.DEVICE = torch.device("cpu")
+    cfg.DROPOUT_P = 0.0
+    train, val = cli_data(cfg)
+    torch.manual_seed(1234)
+    tl = DataLoader(CEOFirmDataset(train), batch_size=256, shuffle=True)
+    vl = DataLoader(CEOFirmDataset(val), batch_size=256, shuffle=False)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf), pytest.warns(RuntimeWarning):
+        model = train_model(tl, vl, train, cfg)
+    lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("Epoch")]
+    assert lines == list(g["printed"])
+    sd = model.state_dict()
+    for k, ref in ((k[len("final/"):], v) for k, v in g.items() if k.startswith("final/")):
+        if excluded_param(k):
+            continue
+        got = sd[k].numpy()
+        if got.dtype.kind == "i":
+            assert np.array_equal(got, ref), k
+        else:
+            assert normwise(got, ref) < 1e-5, k
+
+
+def test_cli_synthetic_runs(tmp_path):
+    env = dict(os.environ, PYTHONPATH=PKG_PARENT, CEO_TT_OUTPUT=str(tmp_path), HIP_VISIBLE_DEVICES="")
+    out = tmp_path / "sd.pt"
+    r = subprocess.run([sys.executable, "-m", "ceo_firm_matching.cli", "--synthetic", "--epochs", "1",
+                        "--save", str(out)], cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Using SYNTHETIC data..." in r.stdout
+    assert "Train size: 800, Val size: 200" in r.stdout
+    assert "Epoch 0: Avg Train Loss = " in r.stdout
+    sd = torch.load(str(out), weights_only=True)
+    assert "logit_scale" in sd and sd["firm_tower.0.weight"].shape == (64, 204)

@@ -11,7 +11,8 @@ own shard of ceil(10M/N) pairs, one flat-gradient all-reduce over RCCL per
 step).  Prints ONE JSON line on rank 0.
 
 Extra legs (rank 0, N=1 only for the CPU baseline):
-* roofline : per-kernel HIP-event timing of K more steps on the launch stream;
+* roofline : per-kernel HIP-event timing of K more steps on the launch stream
+  (events stamped by each kernel's dispatch via hipExtLaunchKernelGGL);
   the dominant kernel's algorithmic FLOP/s (or bytes/s) vs the MI355X peak;
   HBM traffic from the committed rocprofv3 PMC summary when present.
 * cosine_roofline : the standalone fused L2-norm + cosine + weighted-MSE
@@ -173,7 +174,24 @@ def cosine_roofline(dev, D=128, n=1 << 22, reps=20):
             "frac_of_measured_stream": round(gbs / stream, 4), "pairs_per_s": round(n / (ms * 1e-3), 1)}
 
 
+def _guard_stdout():
+    """Route everything native libraries print to stdout (RCCL prints its
+    version banner there at communicator init) to stderr, and return a
+    writer for the ONE JSON result line on the real stdout."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(os.dup(2), "w")
+    out = os.fdopen(real, "w")
+
+    def emit(line):
+        out.write(line + "\n")
+        out.flush()
+    return emit
+
+
 def main():
+    emit = _guard_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -182,6 +200,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / cosine legs")
+    ap.add_argument("--dp", action="store_true",
+                    help="data-parallel step (all-reduce + Adam) even at world size 1 (tests the N>1 path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,8 +210,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if world > 1 or args.dp:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         pg = dist.group.WORLD
 
     from ceo_firm_matching import CEOFirmMatcher, Config
@@ -214,7 +236,10 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     rows = torch.randperm(shard, device=dev, generator=gen)
 
-    use_graph = (world == 1) and not args.no_graph
+    # hipGraph replay of whole steps at every world size: the RCCL all-reduce
+    # of the data-parallel step is captured with the kernels (no host work
+    # per step); --no-graph launches every step eagerly.
+    use_graph = not args.no_graph
     step_fn = lambda: tr.step_cycle(rows, B, n_batches)  # noqa: E731
     for _ in range(args.warmup):
         step_fn()
@@ -235,9 +260,11 @@ def main():
                 step_fn()
         graph.replay()  # one more warm replay
         torch.cuda.synchronize()
+        if pg is not None:
+            dist.barrier()
 
     tr.pop_loss_sum(read=False)
-    if world > 1:
+    if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -248,10 +275,10 @@ def main():
         for _ in range(args.steps):
             step_fn()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if pg is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -268,7 +295,7 @@ def main():
                 "seed 42), resident in HBM",
         "config": {"workload": f"{args.config}: {n_total} pairs ({shard}/GPU), {nf}x{nc} feats, LATENT={D}, "
                                f"bs={B}/GPU, dropout 0.1, Adam lr 4e-4",
-                   "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
+                   "global_batch": B * world, "parallelism": f"dp{world}" if pg is not None else "single",
                    "graph": bool(graph is not None), "graph_chunk": chunk},
         "mean_loss": round(loss, 5),
     }
@@ -276,26 +303,28 @@ def main():
     if not args.no_extras:
         # ---- per-kernel HIP events on the launch stream (separate pass, K steps)
         st = N.stream_ptr(dev)
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(7)] for _ in range(args.steps)]
+        # 2 events per kernel, stamped by the kernel's own dispatch
+        # (tt_train_step_ev -> hipExtLaunchKernelGGL): kernel-only durations
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(12)] for _ in range(args.steps)]
         for row in evs:
             for e in row:
                 e.record()  # materialise the hipEvent
         torch.cuda.synchronize()
         a = tr.arena
         for k in range(args.steps):
-            arr = (ctypes.c_void_p * 7)(*[e.cuda_event for e in evs[k]])
+            arr = (ctypes.c_void_p * 12)(*[e.cuda_event for e in evs[k]])
             batch = tr._batch(rows, 0, B, cycle=n_batches)
             rc = tr.lib.tt_train_step_ev(tr.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
                                          batch, tr.hp, tr.seed, tr.state.data_ptr(), tr.ws.data_ptr(),
                                          tr.ws_bytes, tr.grad.data_ptr(), tr.exp_avg.data_ptr(),
-                                         tr.exp_avg_sq.data_ptr(), int(world == 1), st, arr)
+                                         tr.exp_avg_sq.data_ptr(), int(pg is None), st, arr)
             N.check(rc, "tt_train_step_ev")
-            if world > 1:
+            if pg is not None:
                 tr.allreduce_and_adam()
         torch.cuda.synchronize()
         per = {}
         for i, name in enumerate(KERNELS):
-            per[name] = sum(evs[k][i].elapsed_time(evs[k][i + 1]) for k in range(args.steps)) / args.steps * 1e3
+            per[name] = sum(evs[k][2 * i].elapsed_time(evs[k][2 * i + 1]) for k in range(args.steps)) / args.steps * 1e3
         fl, by = kernel_work(nf, nc, D, B, a.params.numel(), -(-B // 64))
         dom = max(per, key=per.get)
         t_s = per[dom] * 1e-6
@@ -321,8 +350,8 @@ def main():
     else:
         result["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
+        emit(json.dumps(result))
+    if pg is not None:
         dist.destroy_process_group()
 
 

@@ -33,9 +33,11 @@ def world_of(group=None) -> int:
 
 def average_gradients_(flat_grad: torch.Tensor, group=None) -> torch.Tensor:
     """In-place mean over ranks of the flat gradient arena (one collective)."""
-    w = world_of(group)
+    if not (dist.is_available() and dist.is_initialized()):
+        return flat_grad
+    w = dist.get_world_size(group)
+    dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
     if w > 1:
-        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
         flat_grad.mul_(1.0 / w)
     return flat_grad
 

@@ -45,7 +45,10 @@ class FusedTrainer:
         self.hp = N.adam_hp(lr, betas, eps)
         self.seed = (int(torch.cuda.initial_seed()) if seed is None else int(seed)) & ((1 << 63) - 1)
         self.pg = process_group
-        self.world = world_of(process_group) if process_group is not None else 1
+        # data-parallel step (grad -> all-reduce -> Adam) whenever a process
+        # group is given, also at world size 1 (exercises the N > 1 path)
+        self.dp = process_group is not None
+        self.world = world_of(process_group) if self.dp else 1
         if self.world > 1:  # DDP construction semantics: rank 0's state everywhere
             broadcast_state_(self.arena.params, self.arena.buffers, process_group)
         self.max_batch = 0
@@ -105,7 +108,7 @@ class FusedTrainer:
     def step(self, rows: Optional[torch.Tensor], row0: int, n_rows: int):
         """One optimizer step on dataset rows rows[row0:row0+n_rows]."""
         batch = self._batch(rows, row0, n_rows)
-        if self.world == 1:
+        if not self.dp:
             self._launch(batch, n_rows, True)
         else:
             self._launch(batch, n_rows, False)
@@ -117,7 +120,7 @@ class FusedTrainer:
         ``rows`` taken from the device step counter (no host arguments change
         between steps)."""
         batch = self._batch(rows, 0, batch_size, cycle=n_batches, t_base=t_base)
-        if self.world == 1:
+        if not self.dp:
             self._launch(batch, batch_size, True)
         else:
             self._launch(batch, batch_size, False)

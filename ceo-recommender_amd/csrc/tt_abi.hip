@@ -5,6 +5,8 @@
 #include <cstring>
 #include <mutex>
 
+#include <hip/hip_ext.h>
+
 #include "tt_common.h"
 #include "tt_tower.hip"
 #include "tt_optim.hip"
@@ -339,28 +341,43 @@ static int prepare(const tt_model_desc* d, const tt_batch* b, int64_t ws_bytes, 
   return TT_OK;
 }
 
-static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s) {
-  hipLaunchKernelGGL(k_l0_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l0, s, a);
+// Kernel launch with optional profiling events: when (e0, e1) are given the
+// kernel goes through hipExtLaunchKernelGGL, which stamps e0/e1 from the
+// kernel's own dispatch packet (start / end of the kernel, no gap), so
+// bench.py's HIP-event timing is the kernel duration rocprofv3 reports.
+struct Evs {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+template <typename K, typename... A>
+static void launch(K kern, dim3 g, dim3 b, size_t lds, hipStream_t s, Evs ev, A... args) {
+  if (ev.e0 && ev.e1)
+    hipExtLaunchKernelGGL(kern, g, b, (uint32_t)lds, s, ev.e0, ev.e1, 0, args...);
+  else
+    hipLaunchKernelGGL(kern, g, b, lds, s, args...);
 }
-static void launch_l4(const StepArgs& a, const Plan& P, hipStream_t s) {
-  hipLaunchKernelGGL(k_l4_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l4, s, a);
+
+static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
+  launch(k_l0_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l0, s, ev, a);
 }
-static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s) {
-  hipLaunchKernelGGL(k_bwd_mid<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_mid, s, a);
+static void launch_l4(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
+  launch(k_l4_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l4, s, ev, a);
 }
-static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s) {
-  hipLaunchKernelGGL(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, a);
+static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
+  launch(k_bwd_mid<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_mid, s, ev, a);
 }
-static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s) {
+static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
+  launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
+}
+static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev = {}) {
   const dim3 grid(P.n_tiles_top, grid_y), blk(4 * P.top_rows);
   if (P.ndt == 4 && P.top_rows == 64)
-    hipLaunchKernelGGL((k_top<4, 64>), grid, blk, P.lds_top, s, a);
+    launch(k_top<4, 64>, grid, blk, P.lds_top, s, ev, a);
   else if (P.ndt == 4)
-    hipLaunchKernelGGL((k_top<4, 128>), grid, blk, P.lds_top, s, a);
+    launch(k_top<4, 128>, grid, blk, P.lds_top, s, ev, a);
   else if (P.top_rows == 64)
-    hipLaunchKernelGGL((k_top<8, 64>), grid, blk, P.lds_top, s, a);
+    launch(k_top<8, 64>, grid, blk, P.lds_top, s, ev, a);
   else
-    hipLaunchKernelGGL((k_top<8, 128>), grid, blk, P.lds_top, s, a);
+    launch(k_top<8, 128>, grid, blk, P.lds_top, s, ev, a);
 }
 
 }  // namespace tt
@@ -476,19 +493,18 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   a.mode = TOP_TRAIN;
   a.loss_sum = &state->loss_sum;
   auto ev = [&](int k) {
-    if (events && events[k]) (void)hipEventRecord((hipEvent_t)events[k], s);
+    Evs e;
+    if (events) {
+      e.e0 = (hipEvent_t)events[2 * k];
+      e.e1 = (hipEvent_t)events[2 * k + 1];
+    }
+    return e;
   };
-  ev(0);
-  launch_l0(a, c.P, s);
-  ev(1);
-  launch_l4(a, c.P, s);
-  ev(2);
-  launch_top(a, c.P, 2, s);
-  ev(3);
-  launch_mid(a, c.P, s);
-  ev(4);
-  launch_first(a, c.P, s);
-  ev(5);
+  launch_l0(a, c.P, s, ev(0));
+  launch_l4(a, c.P, s, ev(1));
+  launch_top(a, c.P, 2, s, ev(2));
+  launch_mid(a, c.P, s, ev(3));
+  launch_first(a, c.P, s, ev(4));
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   for (int t = 0; t < 2; ++t) {
     r.zero_buf[2 * t] = w + c.W.st0[t];
@@ -508,8 +524,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     r.state = state;
   }
   const int nb = (int)((c.L.n + RED_E - 1) / RED_E);
-  hipLaunchKernelGGL(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, r);
-  ev(6);
+  launch(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, ev(5), r);
   return launch_check();
 }
 

@@ -138,10 +138,12 @@ int32_t tt_train_step(const tt_model_desc* d, float* params, float* buffers, int
                       void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
                       int32_t apply_adam, tt_stream_t stream);
 
-/* tt_train_step with per-kernel timing: when events != NULL, events[k]
- * (a hipEvent_t, or NULL to skip) is recorded on `stream` before kernel k of
- * the step (k = 0..5: l0_fwd, l4_fwd, top, bwd_mid, bwd_first, reduce_adam)
- * and events[6] after the last one.  Used by bench.py's roofline leg.       */
+/* tt_train_step with per-kernel timing: when events != NULL, kernel k of the
+ * step (k = 0..5: l0_fwd, l4_fwd, top, bwd_mid, bwd_first, reduce_adam) is
+ * launched with hipExtLaunchKernelGGL(..., events[2k], events[2k+1]) (two
+ * hipEvent_t, or NULL to launch it plainly): the events are stamped from the
+ * kernel's own dispatch, i.e. they bracket exactly its execution (what
+ * rocprofv3 --kernel-trace reports).  Used by bench.py's roofline leg.      */
 int32_t tt_train_step_ev(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
                          const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state,
                          void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,

@@ -21,6 +21,13 @@ Fixtures:
   * ``cli.npz``: the default CLI pipeline (cli.py:29-59) with dropout
       disabled and EPOCHS=6 under torch.manual_seed(1234): the transformed
       train tensors, printed loss lines and final state_dict.
+  * ``contrastive.npz``: ``info_nce_loss``
+      (contrastive.py:102-138) loss + autograd dF/dC for normalised and
+      un-normalised inputs, B in {1, 2, 64, 256}; ``get_embeddings`` +
+      ``compute_retrieval_metrics`` (contrastive.py:52-72, 275-332) of a
+      small ContrastiveCEOFirmMatcher (the embeddings are stored too).
+
+    python tests/golden/make_golden.py [contrastive]   # only that fixture
 """
 import contextlib
 import io
@@ -299,8 +306,68 @@ def gen_cli():
     print("wrote cli.npz:", lines)
 
 
+def gen_contrastive():
+    from ceo_firm_matching.contrastive import (ContrastiveCEOFirmMatcher, compute_retrieval_metrics,
+                                               info_nce_loss)
+    out = {}
+    g = torch.Generator().manual_seed(5)
+    cases = {"b1": (1, 32, True), "b2": (2, 32, True), "b64": (64, 32, True),
+             "b256": (256, 256, True), "raw256": (256, 256, False)}
+    for name, (B, D, norm) in cases.items():
+        f = torch.randn(B, D, generator=g)
+        c = torch.randn(B, D, generator=g)
+        if norm:
+            f = torch.nn.functional.normalize(f, dim=1)
+            c = torch.nn.functional.normalize(c, dim=1)
+        else:
+            f, c = 0.1 * f, 0.1 * c
+        f.requires_grad_(True)
+        c.requires_grad_(True)
+        loss = info_nce_loss(f, c, 0.07)
+        out[f"nce/{name}/f"] = f.detach().numpy().copy()
+        out[f"nce/{name}/c"] = c.detach().numpy().copy()
+        out[f"nce/{name}/loss"] = np.float32(loss.item())
+        if loss.requires_grad and B <= 64:
+            loss.backward()
+            out[f"nce/{name}/df"] = f.grad.numpy().copy()
+            out[f"nce/{name}/dc"] = c.grad.numpy().copy()
+        # fp64 truth for the tolerance check
+        f64 = f.detach().double().requires_grad_(True)
+        c64 = c.detach().double().requires_grad_(True)
+        l64 = info_nce_loss(f64, c64, 0.07)
+        out[f"nce/{name}/loss64"] = np.float64(l64.item())
+        if l64.requires_grad:
+            l64.backward()
+            # fp64 truth, stored rounded to fp32 (6e-8 relative: far below 1e-5)
+            out[f"nce/{name}/df64"] = f64.grad.numpy().astype(np.float32)
+            out[f"nce/{name}/dc64"] = c64.grad.numpy().astype(np.float32)
+    # retrieval metrics of a small contrastive model (meta_test geometry)
+    cfg = make_config(32)
+    cfg.DEVICE = torch.device("cpu")
+    torch.manual_seed(11)
+    model = ContrastiveCEOFirmMatcher(META_TEST, cfg)
+    rng = np.random.default_rng(11)
+    N = 300
+    bnp = make_batch(META_TEST, N, rng)
+    dd = {k: torch.from_numpy(v) for k, v in bnp.items()}
+    metrics = compute_retrieval_metrics(model, dd, cfg)
+    model.eval()
+    with torch.no_grad():
+        fe, ce = model.get_embeddings(dd["firm_numeric"], dd["firm_cat"], dd["ceo_numeric"], dd["ceo_cat"])
+    out["ret/firm_emb"] = fe.numpy().copy()
+    out["ret/ceo_emb"] = ce.numpy().copy()
+    for k, v in metrics.items():
+        out[f"ret/metric/{k}"] = np.float64(v)
+    np.savez_compressed(os.path.join(HERE, "contrastive.npz"), **out)
+    print("wrote contrastive.npz:", {k: out[f"nce/{k}/loss"] for k in cases}, metrics)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["contrastive"]:
+        gen_contrastive()
+        sys.exit(0)
     for name, (meta, latent, B) in CASES.items():
         gen_case(name, meta, latent, B)
     gen_ddp()
     gen_cli()
+    gen_contrastive()

@@ -30,7 +30,9 @@ _PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("CEO_TT_LIB") or os.path.join(_PKG_PARENT, "lib", "libceo_tt.so")
 EXPORTED = ("tt_abi_version", "tt_param_count", "tt_param_offsets", "tt_buffer_count",
             "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_train_step", "tt_train_step_ev",
-            "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd")
+            "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
+            "tt_nce_workspace_bytes", "tt_nce_norms", "tt_nce_forward", "tt_nce_loss", "tt_nce_backward",
+            "tt_rank_workspace_bytes", "tt_retrieval_ranks")
 
 
 class NativeLibraryError(RuntimeError):
@@ -93,6 +95,13 @@ def lib() -> ctypes.CDLL:
         "tt_adam_apply": (I32, [P, P, P, P, I64, H, P, I64, P]),
         "tt_cosine_forward": (I32, [P, P, I64, I32, P, P, P]),
         "tt_cosine_mse_fwd_bwd": (I32, [P, P, P, P, I64, I32, P, F, P, P, P, P, P, P]),
+        "tt_nce_workspace_bytes": (I64, [I64, I64, I32]),
+        "tt_nce_norms": (I32, [P, P, I64, I64, I32, P, P]),
+        "tt_nce_forward": (I32, [P, P, I64, I64, I32, I64, F, P, P, I64, P, P]),
+        "tt_nce_loss": (I32, [I64, I64, I32, I64, I64, F, P, I64, P, P, P, P]),
+        "tt_nce_backward": (I32, [P, P, I64, I64, I32, I64, I64, F, P, I64, P, P, P]),
+        "tt_rank_workspace_bytes": (I64, [I64]),
+        "tt_retrieval_ranks": (I32, [P, P, I64, I64, I32, I64, P, I64, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,263 @@
+"""Contrastive scoring on the HIP kernels (reference ``contrastive.py``).
+
+SURVEY 8a rows a18/a19, BASELINE cfg 5:
+
+* ``info_nce_loss(firm_proj, ceo_proj, temperature)`` -- same signature and
+  semantics as the reference (contrastive.py:102-138): symmetric InfoNCE over
+  the full B x B similarity matrix, ``B <= 1`` returns 0.  On HIP tensors the
+  forward and backward run in ``libceo_tt.so`` (tt_nce_*: three fp32 MFMA
+  GEMMs, the similarity matrix is never materialised as logits).
+* ``info_nce_loss_sharded`` -- the same loss when the B pairs are sharded over
+  the ranks of a process group (one GPU each): all-gather of the CEO rows,
+  all-reduce of the column sums and of the loss, reduce-scatter of dC.
+* ``retrieval_ranks`` / ``compute_retrieval_metrics`` (contrastive.py:275-332):
+  rank of the true match among all candidates, recall@1/5/k, MRR, median rank.
+* ``ContrastiveCEOFirmMatcher`` (contrastive.py:21-99): the reference's module
+  tree (base CEOFirmMatcher + projector heads) so ``get_embeddings`` callers
+  work unchanged.
+
+On CPU tensors every function evaluates the reference's ATen expression.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native as N
+from .config import Config
+from .model import CEOFirmMatcher
+
+def _check_status(status: torch.Tensor):
+    bad = int(status.item())
+    if bad:
+        raise NotImplementedError(
+            f"info_nce_loss: {bad} softmax sums underflowed; the fused kernels share one exponent shift "
+            "(max|f| max|c| / temperature) and expect (near-)L2-normalised projections")
+
+
+def _f32(x: torch.Tensor) -> torch.Tensor:
+    x = x.to(torch.float32)
+    return x if x.is_contiguous() else x.contiguous()
+
+
+class _NCE:
+    """Host state of one forward (workspace holds E for the backward)."""
+
+    def __init__(self, f, c, m, n, d, row0, batch, tau):
+        self.L = N.lib()
+        self.f, self.c, self.m, self.n, self.d = f, c, m, n, d
+        self.row0, self.batch, self.tau = row0, batch, tau
+        self.ws_bytes = int(self.L.tt_nce_workspace_bytes(m, n, d))
+        if self.ws_bytes < 0:
+            N.check(self.ws_bytes, "tt_nce_workspace_bytes")
+        self.ws = torch.empty(self.ws_bytes // 4, dtype=torch.float32, device=f.device)
+        self.st = N.stream_ptr(f.device)
+
+    def norms(self):
+        norm2 = torch.empty(2, dtype=torch.float32, device=self.f.device)
+        N.check(self.L.tt_nce_norms(self.f.data_ptr(), self.c.data_ptr(), self.m, self.n, self.d,
+                                    norm2.data_ptr(), self.st), "tt_nce_norms")
+        return norm2
+
+    def forward(self, norm2):
+        col_sum = torch.empty(self.n, dtype=torch.float32, device=self.f.device)
+        N.check(self.L.tt_nce_forward(self.f.data_ptr(), self.c.data_ptr(), self.m, self.n, self.d, self.row0,
+                                      ctypes.c_float(self.tau), norm2.data_ptr(), self.ws.data_ptr(),
+                                      self.ws_bytes, col_sum.data_ptr(), self.st), "tt_nce_forward")
+        return col_sum
+
+    def loss(self, col_sum):
+        """(loss share, status): status counts underflowed softmax sums."""
+        loss = torch.zeros(1, dtype=torch.float32, device=self.f.device)
+        status = torch.zeros(1, dtype=torch.int32, device=self.f.device)
+        N.check(self.L.tt_nce_loss(self.m, self.n, self.d, self.row0, self.batch, ctypes.c_float(self.tau),
+                                   self.ws.data_ptr(), self.ws_bytes, col_sum.data_ptr(), loss.data_ptr(),
+                                   status.data_ptr(), self.st), "tt_nce_loss")
+        return loss, status
+
+    def backward(self):
+        df = torch.empty(self.m, self.d, dtype=torch.float32, device=self.f.device)
+        dc = torch.empty(self.n, self.d, dtype=torch.float32, device=self.f.device)
+        N.check(self.L.tt_nce_backward(self.f.data_ptr(), self.c.data_ptr(), self.m, self.n, self.d, self.row0,
+                                       self.batch, ctypes.c_float(self.tau), self.ws.data_ptr(), self.ws_bytes,
+                                       df.data_ptr(), dc.data_ptr(), self.st), "tt_nce_backward")
+        return df, dc
+
+
+class _InfoNCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f, c, temperature):
+        f32, c32 = _f32(f), _f32(c)
+        B, d = f32.shape
+        h = _NCE(f32, c32, B, B, d, 0, B, float(temperature))
+        loss, status = h.loss(h.forward(h.norms()))
+        _check_status(status)
+        ctx.h = h
+        ctx.dtypes = (f.dtype, c.dtype)
+        return loss.reshape(()).to(f.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        df, dc = ctx.h.backward()
+        ctx.h = None  # release E
+        g = g.to(torch.float32)
+        return (df * g).to(ctx.dtypes[0]), (dc * g).to(ctx.dtypes[1]), None
+
+
+def info_nce_loss(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, temperature: float = 0.07) -> torch.Tensor:
+    """Symmetric InfoNCE (reference contrastive.py:102-138)."""
+    B = firm_proj.size(0)
+    if B <= 1:
+        return torch.tensor(0.0, device=firm_proj.device)
+    if firm_proj.device.type == "cuda":
+        if firm_proj.shape != ceo_proj.shape:
+            raise ValueError("info_nce_loss: firm_proj and ceo_proj must have the same shape")
+        return _InfoNCEFn.apply(firm_proj, ceo_proj, temperature)
+    sim_matrix = torch.mm(firm_proj, ceo_proj.t()) / temperature
+    labels = torch.arange(B, device=firm_proj.device)
+    return (F.cross_entropy(sim_matrix, labels) + F.cross_entropy(sim_matrix.t(), labels)) / 2
+
+
+class _ShardedNCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f, c, temperature, group):
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        f32, c32 = _f32(f), _f32(c)
+        m, d = f32.shape
+        if dist.get_backend(group) == "gloo":
+            parts = [torch.empty_like(c32) for _ in range(world)]
+            dist.all_gather(parts, c32, group=group)
+            c_all = torch.cat(parts)
+        else:
+            c_all = torch.empty(world * m, d, dtype=torch.float32, device=f.device)
+            dist.all_gather_into_tensor(c_all, c32, group=group)
+        n = world * m
+        h = _NCE(f32, c_all, m, n, d, rank * m, n, float(temperature))
+        norm2 = h.norms()
+        dist.all_reduce(norm2, op=dist.ReduceOp.MAX, group=group)
+        col_sum = h.forward(norm2)
+        dist.all_reduce(col_sum, group=group)
+        loss, status = h.loss(col_sum)
+        dist.all_reduce(loss, group=group)
+        dist.all_reduce(status, group=group)
+        _check_status(status)
+        ctx.h, ctx.group, ctx.m = h, group, m
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        df, dc_all = ctx.h.backward()
+        ctx.h = None
+        group, m = ctx.group, ctx.m
+        rank = dist.get_rank(group)
+        if dist.get_backend(group) == "gloo":  # no reduce_scatter on gloo
+            dist.all_reduce(dc_all, group=group)
+            dc = dc_all[rank * m:(rank + 1) * m].contiguous()
+        else:
+            dc = torch.empty(m, dc_all.shape[1], dtype=torch.float32, device=dc_all.device)
+            dist.reduce_scatter_tensor(dc, dc_all, group=group)
+        g = g.to(torch.float32)
+        return df * g, dc * g, None, None
+
+
+def info_nce_loss_sharded(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, temperature: float = 0.07,
+                          group=None) -> torch.Tensor:
+    """InfoNCE over pairs sharded across the ranks of ``group`` (equal shards:
+    rank r holds pairs [r*m, (r+1)*m)).  Returns the global loss on every rank;
+    gradients flow to the local shards."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return info_nce_loss(firm_proj, ceo_proj, temperature)
+    if firm_proj.device.type != "cuda":
+        raise NotImplementedError("info_nce_loss_sharded runs on the HIP kernels (one GPU per rank)")
+    return _ShardedNCEFn.apply(firm_proj, ceo_proj, temperature, group)
+
+
+# --------------------------------------------------------------------------
+# retrieval
+# --------------------------------------------------------------------------
+def retrieval_ranks_rows(f: torch.Tensor, c: torch.Tensor, row0: int = 0) -> torch.Tensor:
+    """1-based rank of the true match (ceo row row0 + i) of each firm row i
+    among all rows of ``c`` (a row shard of firms against every CEO)."""
+    m, n = f.shape[0], c.shape[0]
+    if row0 < 0 or row0 + m > n:
+        raise ValueError("retrieval_ranks_rows: firm rows must map onto ceo rows row0..row0+m")
+    if f.device.type != "cuda":
+        sim = f.double() @ c.double().t()
+        idx = torch.arange(m)
+        d = sim[idx, row0 + idx]
+        gt = sim > d[:, None]
+        gt[idx, row0 + idx] = False
+        return gt.sum(dim=1).to(torch.int32) + 1
+    f32, c32 = _f32(f), _f32(c)
+    L = N.lib()
+    wsb = int(L.tt_rank_workspace_bytes(m))
+    if wsb < 0:
+        N.check(wsb, "tt_rank_workspace_bytes")
+    ws = torch.empty(wsb // 4, dtype=torch.float32, device=f.device)
+    ranks = torch.empty(m, dtype=torch.int32, device=f.device)
+    N.check(L.tt_retrieval_ranks(f32.data_ptr(), c32.data_ptr(), m, n, f32.shape[1], row0, ws.data_ptr(), wsb,
+                                 ranks.data_ptr(), N.stream_ptr(f.device)), "tt_retrieval_ranks")
+    return ranks
+
+
+def retrieval_ranks(firm_emb: torch.Tensor, ceo_emb: torch.Tensor, cap: Optional[int] = 5000) -> torch.Tensor:
+    """Ranks over the first N = min(rows, cap) pairs, as the reference
+    (contrastive.py:306-322); ``cap=None`` ranks all pairs."""
+    N_ = firm_emb.size(0) if cap is None else min(firm_emb.size(0), cap)
+    return retrieval_ranks_rows(firm_emb[:N_], ceo_emb[:N_], 0)
+
+
+def metrics_from_ranks(ranks: torch.Tensor, top_k: int = 10) -> Dict[str, float]:
+    r = ranks.detach().cpu().numpy().astype(np.float64)
+    return {
+        'recall@1': float(np.mean(r <= 1)),
+        'recall@5': float(np.mean(r <= 5)),
+        'recall@10': float(np.mean(r <= top_k)),
+        'MRR': float(np.mean(1.0 / r)),
+        'median_rank': float(np.median(r)),
+    }
+
+
+def compute_retrieval_metrics(model, data_dict: Dict, config: Config, top_k: int = 10,
+                              cap: Optional[int] = 5000) -> Dict[str, float]:
+    """Reference contrastive.py:275-332 (``cap=None``: no 5000-row cap)."""
+    model.eval()
+    with torch.no_grad():
+        dev = config.DEVICE
+        fe, ce = model.get_embeddings(data_dict['firm_numeric'].to(dev), data_dict['firm_cat'].to(dev),
+                                      data_dict['ceo_numeric'].to(dev), data_dict['ceo_cat'].to(dev))
+        ranks = retrieval_ranks(fe, ce, cap=cap)
+    return metrics_from_ranks(ranks, top_k)
+
+
+# --------------------------------------------------------------------------
+# module tree of the reference (contrastive.py:21-99)
+# --------------------------------------------------------------------------
+class ContrastiveCEOFirmMatcher(nn.Module):
+    def __init__(self, metadata: Dict[str, int], config: Config):
+        super().__init__()
+        self.base_model = CEOFirmMatcher(metadata, config)
+        self.config = config
+        D = config.LATENT_DIM
+        self.firm_projector = nn.Sequential(nn.Linear(D, D), nn.ReLU(), nn.Linear(D, D // 2))
+        self.ceo_projector = nn.Sequential(nn.Linear(D, D), nn.ReLU(), nn.Linear(D, D // 2))
+
+    def get_embeddings(self, f_numeric, f_cat, c_numeric, c_cat):
+        b = self.base_model
+        f_embs = [emb(f_cat[:, i]) for i, emb in enumerate(b.firm_embeddings)]
+        u = b.firm_tower(torch.cat([f_numeric] + f_embs, dim=1))
+        c_embs = [emb(c_cat[:, i]) for i, emb in enumerate(b.ceo_embeddings)]
+        v = b.ceo_tower(torch.cat([c_numeric] + c_embs, dim=1))
+        return F.normalize(u, dim=1), F.normalize(v, dim=1)
+
+    def forward(self, f_numeric, f_cat, c_numeric, c_cat):
+        u, v = self.get_embeddings(f_numeric, f_cat, c_numeric, c_cat)
+        match_score = (u * v).sum(dim=1, keepdim=True) * self.base_model.logit_scale.exp()
+        return match_score, F.normalize(self.firm_projector(u), dim=1), F.normalize(self.ceo_projector(v), dim=1)

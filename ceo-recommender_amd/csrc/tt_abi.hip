@@ -11,6 +11,7 @@
 #include "tt_tower.hip"
 #include "tt_optim.hip"
 #include "tt_cosine.hip"
+#include "tt_contrastive.hip"
 
 #ifdef TT_STAMPS
 namespace tt {
@@ -604,6 +605,249 @@ int32_t tt_cosine_mse_fwd_bwd(const float* u, const float* v, const float* targe
                               float* dv, float* loss_sum, float* dls_sum, tt_stream_t stream) {
   return cosine_launch(u, v, target, weight, B, D, logit_scale, inv_batch, score, du, dv, loss_sum, dls_sum, true,
                        (hipStream_t)stream);
+}
+
+
+// ---------------------------------------------------------------------------
+// Contrastive (InfoNCE / retrieval): tt_nce_*, tt_retrieval_ranks
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace tt {
+namespace nce {
+
+struct NceLayout {
+  int64_t m, n, m_pad, n_pad, nti, ntj;
+  int64_t n_bm, n_bn;       // sim GEMM blocks
+  int64_t n_rp, n_cp;       // row / column partial counts
+  int64_t d_pad, pntj;      // grad outputs: columns (D) in 16-tiles
+  int64_t split_f, kps_f;   // dF = E' C   (K = n_pad)
+  int64_t split_c, kps_c;   // dC = E'^T F (K = m_pad)
+  int64_t E, rowpart, colpart, rowsum, diag, a, b, shift, part, total;  // float offsets
+};
+
+static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// split-K so a grad GEMM launches >= ~4 blocks per CU; each split >= 8 K chunks
+static void pick_split(int64_t out_rows, int64_t d, int64_t K, int64_t* split, int64_t* kps) {
+  const int64_t blocks = ((out_rows + BM - 1) / BM) * ((d + BN - 1) / BN);
+  int64_t s = std::max<int64_t>(1, (1024 + blocks - 1) / blocks);
+  const int64_t chunks = (K + BK - 1) / BK;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, chunks / 8));
+  *kps = rup((chunks + s - 1) / s, 1) * BK;
+  *split = (K + *kps - 1) / *kps;
+}
+
+static NceLayout nce_layout(int64_t m, int64_t n, int d) {
+  NceLayout L;
+  L.m = m;
+  L.n = n;
+  L.m_pad = rup(std::max<int64_t>(m, 1), 16);
+  L.n_pad = rup(std::max<int64_t>(n, 1), 16);
+  L.nti = L.m_pad / 16;
+  L.ntj = L.n_pad / 16;
+  L.n_bm = (m + BM - 1) / BM;
+  L.n_bn = (n + BN - 1) / BN;
+  L.n_rp = L.n_bn * NWN;
+  L.n_cp = L.n_bm * NWM;
+  L.d_pad = rup(d, 16);
+  L.pntj = L.d_pad / 16;
+  pick_split(m, d, L.n_pad, &L.split_f, &L.kps_f);
+  pick_split(n, d, L.m_pad, &L.split_c, &L.kps_c);
+  int64_t off = 0;
+  auto take = [&](int64_t k) { const int64_t o = off; off += rup(k, 64); return o; };
+  L.E = take(L.nti * L.ntj * TILE);
+  L.rowpart = take(L.n_rp * L.m_pad);
+  L.colpart = take(L.n_cp * L.n_pad);
+  L.rowsum = take(L.m_pad);
+  L.diag = take(L.m_pad);
+  L.a = take(L.m_pad);
+  L.b = take(L.n_pad);
+  L.shift = take(1);
+  L.part = take(std::max(L.split_f * L.nti, L.split_c * L.ntj) * L.pntj * TILE);
+  L.total = off;
+  return L;
+}
+
+static bool nce_args_ok(const float* f, const float* c, int64_t m, int64_t n, int d, int64_t row0) {
+  if (!f || !c || m < 1 || n < 1 || d < 4 || d % 4) return false;
+  if ((uintptr_t)f % 16 || (uintptr_t)c % 16) return false;
+  return row0 >= 0 && row0 + m <= n;
+}
+
+static std::once_flag g_nce_attr;
+static void nce_attrs() {
+  std::call_once(g_nce_attr, [] {
+    const void* ks[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>,
+                        (const void*)k_nce_dgrad<SRC_E_AS_KM>, (const void*)k_nce_dgrad<SRC_E_AS_MK>};
+    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
+  });
+}
+
+static GemmArgs sim_args(const float* f, const float* c, int64_t m, int64_t n, int d, int64_t row0) {
+  GemmArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.A = Opnd{f, d, m, d, 0, 0, nullptr, nullptr};
+  g.B = Opnd{c, d, n, d, 0, 0, nullptr, nullptr};
+  g.M = m;
+  g.N = n;
+  g.n_blocks_n = (int)((n + BN - 1) / BN);
+  g.row0 = row0;
+  return g;
+}
+
+}  // namespace nce
+}  // namespace tt
+
+extern "C" {
+
+int64_t tt_nce_workspace_bytes(int64_t m, int64_t n, int32_t d) {
+  if (m < 1 || n < 1 || d < 4 || d % 4) return TT_ERR_ARG;
+  return tt::nce::nce_layout(m, n, d).total * (int64_t)sizeof(float);
+}
+
+int32_t tt_nce_norms(const float* f, const float* c, int64_t m, int64_t n, int32_t d, float* norm2,
+                     tt_stream_t stream) {
+  if (!f || !c || !norm2 || m < 1 || n < 1 || d < 1) return TT_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  (void)hipMemsetAsync(norm2, 0, 2 * sizeof(float), s);
+  const int64_t groups = (m + n + 15) / 16;
+  const int nb = (int)std::min<int64_t>(groups, 4096);
+  hipLaunchKernelGGL(tt::nce::k_nce_norms, dim3(nb), dim3(256), 0, s, f, c, m, n, d, norm2);
+  return launch_check();
+}
+
+int32_t tt_nce_forward(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                       float temperature, const float* norm2, void* ws, int64_t ws_bytes, float* col_sum,
+                       tt_stream_t stream) {
+  using namespace tt::nce;
+  if (!nce_args_ok(f, c, m, n, d, row0) || !norm2 || !ws || !col_sum || !(temperature > 0.f)) return TT_ERR_ARG;
+  const NceLayout L = nce_layout(m, n, d);
+  if (L.total * (int64_t)sizeof(float) > ws_bytes) return TT_ERR_WORKSPACE;
+  nce_attrs();
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  const float inv_tau = 1.0f / temperature;
+  hipLaunchKernelGGL(k_nce_set_shift, dim3(1), dim3(64), 0, s, norm2, inv_tau, w + L.shift);
+  hipLaunchKernelGGL(k_nce_diag, dim3((unsigned)((L.nti + 3) / 4)), dim3(256), 0, s, f, c, m, n, d, row0, inv_tau,
+                     w + L.diag);
+  GemmArgs g = sim_args(f, c, m, n, d, row0);
+  g.inv_tau = inv_tau;
+  g.shift = w + L.shift;
+  g.E = w + L.E;
+  g.e_nti = L.nti;
+  g.e_ntj = L.ntj;
+  g.rowpart = w + L.rowpart;
+  g.colpart = w + L.colpart;
+  g.m_pad = L.m_pad;
+  g.n_pad = L.n_pad;
+  hipLaunchKernelGGL(k_nce_sim<0>, dim3((unsigned)(L.n_bm * L.n_bn)), dim3(NTH), LDS_BYTES, s, g);
+  const int64_t tot = L.m_pad + L.n_pad;
+  const int nb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_nce_sums, dim3(nb), dim3(256), 0, s, w + L.rowpart, L.n_rp, L.m_pad, w + L.colpart, L.n_cp,
+                     L.n_pad, w + L.rowsum, w + L.b);
+  // column partial sums of these rows -> caller (n values; all-reduce SUM across row shards)
+  (void)hipMemcpyAsync(col_sum, w + L.b, sizeof(float) * n, hipMemcpyDeviceToDevice, s);
+  return launch_check();
+}
+
+int32_t tt_nce_loss(int64_t m, int64_t n, int32_t d, int64_t row0, int64_t batch, float temperature, void* ws,
+                    int64_t ws_bytes, const float* col_sum, float* loss, int32_t* status, tt_stream_t stream) {
+  using namespace tt::nce;
+  if (m < 1 || n < 1 || d < 4 || !ws || !col_sum || !loss || batch < 2 || row0 < 0 || row0 + m > n)
+    return TT_ERR_ARG;
+  const NceLayout L = nce_layout(m, n, d);
+  if (L.total * (int64_t)sizeof(float) > ws_bytes) return TT_ERR_WORKSPACE;
+  (void)temperature;
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  const int64_t tot = L.m_pad + L.n_pad;
+  const int nb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_nce_loss, dim3(nb), dim3(256), 0, s, w + L.rowsum, col_sum, w + L.diag, m, L.m_pad, n,
+                     L.n_pad, row0, (float)(0.5 / (double)batch), w + L.shift, w + L.a, w + L.b, loss, status);
+  return launch_check();
+}
+
+int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                        int64_t batch, float temperature, void* ws, int64_t ws_bytes, float* df, float* dc,
+                        tt_stream_t stream) {
+  using namespace tt::nce;
+  if (!nce_args_ok(f, c, m, n, d, row0) || !ws || !df || !dc || batch < 2 || !(temperature > 0.f))
+    return TT_ERR_ARG;
+  const NceLayout L = nce_layout(m, n, d);
+  if (L.total * (int64_t)sizeof(float) > ws_bytes) return TT_ERR_WORKSPACE;
+  nce_attrs();
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  const float scale = (float)(1.0 / (2.0 * (double)batch * (double)temperature));
+  const float corr = (float)(1.0 / ((double)batch * (double)temperature));
+  // dF = E' C  (M = m rows i, N = d, K = n_pad columns j)
+  {
+    GemmArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.A = Opnd{w + L.E, 0, m, L.n_pad, L.nti, L.ntj, w + L.a, w + L.b};
+    g.B = Opnd{c, d, d, n, 0, 0, nullptr, nullptr};
+    g.M = m;
+    g.N = d;
+    g.k_per_split = L.kps_f;
+    g.n_blocks_n = (int)((d + BN - 1) / BN);
+    g.part = w + L.part;
+    g.p_nti = L.nti;
+    g.p_ntj = L.pntj;
+    const dim3 grid((unsigned)(((m + BM - 1) / BM) * g.n_blocks_n), (unsigned)L.split_f);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_KM>, grid, dim3(NTH), LDS_BYTES, s, g);
+    const int64_t el = L.nti * L.pntj * 64;
+    hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
+                       s, w + L.part, L.split_f, L.nti, L.pntj, m, d, scale, corr, c, n, row0, df);
+  }
+  // dC = E'^T F  (M = n columns j, N = d, K = m_pad rows i)
+  {
+    GemmArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.A = Opnd{w + L.E, 0, n, L.m_pad, L.nti, L.ntj, w + L.a, w + L.b};
+    g.B = Opnd{f, d, d, m, 0, 0, nullptr, nullptr};
+    g.M = n;
+    g.N = d;
+    g.k_per_split = L.kps_c;
+    g.n_blocks_n = (int)((d + BN - 1) / BN);
+    g.part = w + L.part;
+    g.p_nti = L.ntj;
+    g.p_ntj = L.pntj;
+    const dim3 grid((unsigned)(((n + BM - 1) / BM) * g.n_blocks_n), (unsigned)L.split_c);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(NTH), LDS_BYTES, s, g);
+    const int64_t el = L.ntj * L.pntj * 64;
+    hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
+                       s, w + L.part, L.split_c, L.ntj, L.pntj, n, d, scale, corr, f, m, -row0, dc);
+  }
+  return launch_check();
+}
+
+int64_t tt_rank_workspace_bytes(int64_t m) {
+  if (m < 1) return TT_ERR_ARG;
+  return (int64_t)sizeof(float) * 2 * ((m + 63) / 64 * 64);
+}
+
+int32_t tt_retrieval_ranks(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0, void* ws,
+                           int64_t ws_bytes, int32_t* ranks, tt_stream_t stream) {
+  using namespace tt::nce;
+  if (!nce_args_ok(f, c, m, n, d, row0) || !ws || !ranks) return TT_ERR_ARG;
+  if (tt_rank_workspace_bytes(m) > ws_bytes) return TT_ERR_WORKSPACE;
+  nce_attrs();
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t mp = (m + 63) / 64 * 64;
+  float* diag = (float*)ws;
+  int* cnt = (int*)((float*)ws + mp);
+  (void)hipMemsetAsync(cnt, 0, sizeof(int) * m, s);
+  hipLaunchKernelGGL(k_nce_diag, dim3((unsigned)(((m + 15) / 16 + 3) / 4)), dim3(256), 0, s, f, c, m, n, d, row0,
+                     1.0f, diag);
+  GemmArgs g = sim_args(f, c, m, n, d, row0);
+  g.diag = diag;
+  g.rank_cnt = cnt;
+  const int64_t nblk = ((m + BM - 1) / BM) * g.n_blocks_n;
+  hipLaunchKernelGGL(k_nce_sim<1>, dim3((unsigned)nblk), dim3(NTH), LDS_BYTES, s, g);
+  hipLaunchKernelGGL(k_rank_finish, dim3((unsigned)std::min<int64_t>((m + 255) / 256, 4096)), dim3(256), 0, s, cnt,
+                     m, ranks);
+  return launch_check();
 }
 
 }  // extern "C"

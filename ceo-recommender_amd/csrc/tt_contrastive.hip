@@ -1,0 +1,472 @@
+// Contrastive scoring (gfx950): symmetric InfoNCE forward/backward over the
+// full firm x CEO similarity matrix, and retrieval ranks.
+//
+// Reference: contrastive.py:102-138 (info_nce_loss: S = F C^T / tau,
+// (CE(S, diag) + CE(S^T, diag)) / 2) and contrastive.py:275-332
+// (compute_retrieval_metrics: rank of the diagonal in each row of F C^T).
+// SURVEY 8a rows a18/a19, BASELINE cfg 5 (100k x 100k, D = 256).
+//
+// MFMA-bound: three fp32 GEMMs of 2 M N D flops each (exact fp32 products,
+// v_mfma_f32_16x16x4_f32), never materialising S as logits:
+//   k_nce_sim  : S tile = F C^T (K = D) -> E = exp(S/tau - shift) stored in
+//                16x16 MFMA-accumulator tiles (one coalesced 1 KB store per
+//                tile), deterministic row / column partial sums of E, diag.
+//   k_nce_dgrad: dF = E'C and dC = E'^T F with E' = E (1/rowsum_i +
+//                1/colsum_j), E streamed from HBM (split-K partials).
+//   reduce     : sums, log-sum-exp, loss, diagonal terms, scaling.
+// One shared exponent per element serves both softmaxes: with the fixed
+// shift = max|f| max|c| / tau >= every S_ij, row sums and column sums are
+// plain sums (no running max; column partials of different row blocks and
+// different ranks simply add).  L2-normalised inputs give shift = 1/tau and
+// every term >= exp(-2/tau); sums that still underflow (far-from-normalised
+// inputs) are counted in a status word instead of silently returning inf.
+#include "tt_common.h"
+
+namespace tt {
+namespace nce {
+
+constexpr int BM = 256, BN = 256, BK = 32, WM = 64, WN = 128;
+constexpr int NWM = BM / WM, NWN = BN / WN, NW = NWM * NWN;  // 4 x 2 = 8 waves
+constexpr int NTH = NW * 64;                                 // 512
+constexpr int TM = WM / 16, TN = WN / 16;                    // 4 x 8 MFMA tiles / wave
+constexpr int TILE = 256;                                    // floats per 16x16 tile
+constexpr float SUM_MIN = 1e-30f;  // row/col sums below this: exp underflow (reported)
+
+// LDS operand layouts (floats): "MK" = [m][k] (k contiguous, b128 reads),
+// "KM" = [k][m] (m contiguous, b32 reads).  +4 padding.
+constexpr int LD_MK = BK + 4;
+constexpr int LD_KM = BM + 4;  // BM == BN
+constexpr int OPND_FLOATS = (BM * LD_MK > BK * LD_KM) ? BM * LD_MK : BK * LD_KM;
+constexpr int STAGE_FLOATS = 2 * OPND_FLOATS;  // A + B
+constexpr size_t LDS_BYTES = sizeof(float) * 2 * STAGE_FLOATS;  // double buffered
+
+// Where an operand comes from and how it is laid out in LDS.
+enum Src : int {
+  SRC_MK = 0,       // row-major G[m][k] (ld)            -> LDS [m][k]
+  SRC_KM = 1,       // row-major G[k][m] (ld)            -> LDS [k][m]
+  SRC_E_AS_KM = 2,  // E tiles, m = E row i, k = E col j -> LDS [k][m]  (dF = E' C)
+  SRC_E_AS_MK = 3,  // E tiles, m = E col j, k = E row i -> LDS [m][k]  (dC = E'^T F)
+};
+__host__ __device__ constexpr bool lds_mk(int s) { return s == SRC_MK || s == SRC_E_AS_MK; }
+
+struct Opnd {
+  const float* p;
+  int64_t ld;      // row stride (SRC_MK / SRC_KM)
+  int64_t mdim;    // extent along m (rows of the output side)
+  int64_t kdim;    // extent along k
+  int64_t nti, ntj;  // E tile grid (SRC_E_*)
+  const float* a;  // E row scale (1/rowsum_i, padded)  (SRC_E_*)
+  const float* b;  // E col scale (1/colsum_j, padded)
+};
+
+struct GemmArgs {
+  Opnd A, B;
+  int64_t M, N;        // output extent
+  int64_t k_per_split; // multiple of BK
+  int n_blocks_n;      // blocks along N
+  // sim epilogue
+  float inv_tau;
+  const float* shift;  // device scalar
+  float* E;            // tiles [nti][ntj][256]
+  int64_t e_nti, e_ntj;
+  float* rowpart;      // [N / WN parts][M_pad]
+  float* colpart;      // [M / WM parts][N_pad]
+  int64_t m_pad, n_pad;
+  int64_t row0;        // global index of local row 0 (diagonal j == row0 + i)
+  // rank epilogue
+  const float* diag;   // [M] raw sim_ii (GEMM-identical arithmetic)
+  int* rank_cnt;       // [M]
+  // grad epilogue
+  float* part;         // [split][M_tiles][N_tiles][256]
+  int64_t p_nti, p_ntj;
+};
+
+// ---- global -> registers (4 float4 per thread per operand per K chunk) ----
+template <int S>
+__device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0, float4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = (int)threadIdx.x + q * NTH;
+    if constexpr (S == SRC_MK) {  // tile BM x BK: 8 float4 per row
+      const int r = e >> 3, kq = (e & 7) * 4;
+      const int64_t gm = m0 + r, gk = k0 + kq;
+      const bool ok = gm < o.mdim && gk < o.kdim;
+      const float* p = o.p + (ok ? gm * o.ld + gk : 0);
+      const float4 x = *reinterpret_cast<const float4*>(p);
+      v[q] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if constexpr (S == SRC_KM) {  // tile BK x BM: 64 float4 per k row
+      const int kr = e >> 6, mq = (e & 63) * 4;
+      const int64_t gk = k0 + kr, gm = m0 + mq;
+      const bool ok = gk < o.kdim && gm < o.mdim;
+      const float* p = o.p + (ok ? gk * o.ld + gm : 0);
+      const float4 x = *reinterpret_cast<const float4*>(p);
+      v[q] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {  // E tiles: 32 tiles of 1 KB (16 along m x 2 along k), lane -> float4
+      const int t = e >> 6, ln = e & 63;
+      const int tm = t >> 1, tk = t & 1;
+      int64_t ti, tj;  // E tile coordinates (i = E row block, j = E col block)
+      if constexpr (S == SRC_E_AS_KM) {
+        ti = m0 / 16 + tm;
+        tj = k0 / 16 + tk;
+      } else {
+        tj = m0 / 16 + tm;
+        ti = k0 / 16 + tk;
+      }
+      const bool ok = ti < o.nti && tj < o.ntj;
+      const f32x4 x = __builtin_nontemporal_load(
+          reinterpret_cast<const f32x4*>(o.p + (ok ? (ti * o.ntj + tj) * TILE : 0) + ln * 4));
+      // E' = E (a_i + b_j): rows i = 16 ti + 4 (ln>>4) + s, column j = 16 tj + (ln & 15)
+      const int64_t i0 = (ok ? ti : 0) * 16 + 4 * (ln >> 4);
+      const float4 ai = *reinterpret_cast<const float4*>(o.a + i0);
+      const float bj = o.b[(ok ? tj : 0) * 16 + (ln & 15)];
+      float4 y;
+      y.x = x[0] * (ai.x + bj);
+      y.y = x[1] * (ai.y + bj);
+      y.z = x[2] * (ai.z + bj);
+      y.w = x[3] * (ai.w + bj);
+      v[q] = ok ? y : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+template <int S>
+__device__ __forceinline__ void store_opnd(float* L, const float4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = (int)threadIdx.x + q * NTH;
+    float* d;
+    if constexpr (S == SRC_MK) {
+      d = L + (e >> 3) * LD_MK + (e & 7) * 4;
+    } else if constexpr (S == SRC_KM) {
+      d = L + (e >> 6) * LD_KM + (e & 63) * 4;
+    } else {
+      const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
+      // the lane's float4 runs along E rows i (4 consecutive)
+      if constexpr (S == SRC_E_AS_KM)  // m = i (consecutive), k = j
+        d = L + (16 * tk + (ln & 15)) * LD_KM + 16 * tm + 4 * (ln >> 4);
+      else  // m = j, k = i (consecutive)
+        d = L + (16 * tm + (ln & 15)) * LD_MK + 16 * tk + 4 * (ln >> 4);
+    }
+    *reinterpret_cast<float4*>(d) = v[q];
+  }
+}
+
+// MFMA fragment of a 16-wide K slice: 4 consecutive k (k = kk + 4g + s)
+template <bool MK>
+__device__ __forceinline__ float4 frag(const float* L, int m, int kk, int g) {
+  if constexpr (MK) {
+    return *reinterpret_cast<const float4*>(L + m * LD_MK + kk + 4 * g);
+  } else {
+    const float* p = L + (kk + 4 * g) * LD_KM + m;
+    return make_float4(p[0], p[LD_KM], p[2 * LD_KM], p[3 * LD_KM]);
+  }
+}
+
+// Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T
+template <int SA, int SB>
+__device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
+                                          float* smem, f32x4 (&acc)[TM][TN]) {
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
+  const int wm = w / NWN, wn = w % NWN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  float4 va[4], vb[4];
+  const int nch = (int)((ke - kb + BK - 1) / BK);
+  if (nch <= 0) return;
+  load_opnd<SA>(g_.A, m0, kb, va);
+  load_opnd<SB>(g_.B, n0, kb, vb);
+  store_opnd<SA>(smem, va);
+  store_opnd<SB>(smem + OPND_FLOATS, vb);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    float* cur = smem + (c & 1) * STAGE_FLOATS;
+    if (c + 1 < nch) {
+      load_opnd<SA>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
+      load_opnd<SB>(g_.B, n0, kb + (int64_t)(c + 1) * BK, vb);
+    }
+    const float* As = cur;
+    const float* Bs = cur + OPND_FLOATS;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 16) {
+      float4 a[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = frag<lds_mk(SA)>(As, wm * WM + 16 * i + r, kk, g);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {  // one B fragment live at a time (register budget)
+        const float4 b = frag<lds_mk(SB)>(Bs, wn * WN + 16 * j + r, kk, g);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mfma_k16(a[i], b, acc[i][j]);
+      }
+    }
+    if (c + 1 < nch) {
+      float* nxt = smem + ((c + 1) & 1) * STAGE_FLOATS;
+      store_opnd<SA>(nxt, va);
+      store_opnd<SB>(nxt + OPND_FLOATS, vb);
+    }
+    __syncthreads();
+  }
+}
+
+// XCD-aware block order: consecutive block ids land on different XCDs
+// (round robin); remap so each XCD walks a compact run of the tile grid
+// (shared A/B panels stay in its L2).
+// Bijective: XCD x (= bid % 8) owns logical ids [x*qf + min(x, rem), ...).
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t nblk) {
+  const int64_t qf = nblk / 8, rem = nblk % 8;
+  const int64_t x = bid % 8, q = bid / 8;
+  return x * qf + (x < rem ? x : rem) + q;
+}
+
+// ---------------------------------------------------------------------------
+// k_nce_sim: S = F C^T (MODE 0: InfoNCE exp/partials; MODE 1: rank counts)
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(NTH) void k_nce_sim(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int64_t nblk = (int64_t)gridDim.x;
+  const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
+  const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
+  const int64_t m0 = bm * BM, n0 = bn * BN;
+  f32x4 acc[TM][TN];
+  gemm_loop<SRC_MK, SRC_MK>(a, m0, n0, 0, a.A.kdim, smem, acc);
+
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
+  const int wm = w / NWN, wn = w % NWN;
+  if constexpr (MODE == 0) {
+    const float shift = *a.shift;
+    float rs[TM][4];
+    float cs[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) cs[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rs[i][q] = 0.f;
+      const int64_t ti = (m0 + wm * WM + 16 * i) / 16;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t tj = (n0 + wn * WN + 16 * j) / 16;
+        const int64_t gj = tj * 16 + r;
+        f32x4 e;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t gi = ti * 16 + 4 * g + q;
+          const float s = acc[i][j][q] * a.inv_tau;
+          const bool in = gi < a.M && gj < a.N;
+          e[q] = in ? __expf(s - shift) : 0.f;
+          rs[i][q] += e[q];
+          cs[j] += e[q];
+        }
+        if (ti < a.e_nti && tj < a.e_ntj)
+          __builtin_nontemporal_store(e, reinterpret_cast<f32x4*>(a.E + (ti * a.e_ntj + tj) * TILE) + l);
+      }
+    }
+    // row partials (sum over this wave's WN columns) -> rowpart[part][row]
+    const int64_t rpart = bn * NWN + wn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v = row_reduce16(rs[i][q]);
+        const int64_t gi = m0 + wm * WM + 16 * i + 4 * g + q;
+        if (r == 0 && gi < a.m_pad) a.rowpart[rpart * a.m_pad + gi] = v;
+      }
+    // column partials (sum over this wave's WM rows) -> colpart[part][col]
+    const int64_t cpart = bm * NWM + wm;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float v = col_reduce(cs[j]);
+      const int64_t gj = n0 + wn * WN + 16 * j + r;
+      if (g == 0 && gj < a.n_pad) a.colpart[cpart * a.n_pad + gj] = v;
+    }
+  } else {
+    // rank: count j != row0 + i with sim_ij > sim_ii
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t gi = m0 + wm * WM + 16 * i + 4 * g + q;
+        const float d = a.diag[gi < a.M ? gi : 0];
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int64_t gj = n0 + wn * WN + 16 * j + r;
+          cnt += (gj < a.N && gj != a.row0 + gi && acc[i][j][q] > d) ? 1 : 0;
+        }
+        const float c = row_reduce16((float)cnt);  // exact for counts < 2^24
+        if (r == 0 && gi < a.M && c > 0.f) atomicAdd(a.rank_cnt + gi, (int)c);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// diagonal of F C^T with the GEMM's own arithmetic (same MFMA sequence per
+// 16x16 tile, same K order) -> bitwise the value the tiled GEMM produces.
+// One wave per 16-row tile; C rows row0 + i.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_nce_diag(const float* __restrict__ F, const float* __restrict__ C,
+                                                  int64_t m, int64_t n, int d, int64_t row0, float scale,
+                                                  float* __restrict__ diag) {
+  const int l = lane_id(), r = l & 15, g = l >> 4;
+  const int64_t t = (int64_t)blockIdx.x * 4 + wave_id();
+  const int64_t i = t * 16 + r;  // row of this lane (A operand) and column (B operand)
+  const bool okf = i < m, okc = (row0 + i) < n && (row0 + i) >= 0;
+  f32x4 acc = zero4();
+  for (int k0 = 0; k0 < d; k0 += 16) {
+    const int k = k0 + 4 * g;
+    const bool kk = k < d;
+    float4 av = make_float4(0.f, 0.f, 0.f, 0.f), bv = av;
+    if (okf && kk) av = *reinterpret_cast<const float4*>(F + i * d + k);
+    if (okc && kk) bv = *reinterpret_cast<const float4*>(C + (row0 + i) * d + k);
+    mfma_k16(av, bv, acc);
+  }
+  // acc[q] = C[row 4g+q][col r]; the diagonal is row == col
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (4 * g + q == r && okf && okc) diag[i] = acc[q] * scale;
+}
+
+// ---------------------------------------------------------------------------
+// k_nce_dgrad: split-K partial of  E'^(T) X  (dF: E' C, dC: E'^T F) into
+// accumulator-layout tiles part[split][ti][tj][256]
+// ---------------------------------------------------------------------------
+template <int SA>
+__global__ __launch_bounds__(NTH) void k_nce_dgrad(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int64_t nblk = (int64_t)gridDim.x;
+  const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
+  const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
+  const int64_t m0 = bm * BM, n0 = bn * BN;
+  const int64_t split = blockIdx.y;
+  const int64_t kb = split * a.k_per_split;
+  const int64_t ke = min(kb + a.k_per_split, a.A.kdim);
+  f32x4 acc[TM][TN];
+  gemm_loop<SA, SRC_KM>(a, m0, n0, kb, ke, smem, acc);
+  const int w = wave_id(), l = lane_id();
+  const int wm = w / NWN, wn = w % NWN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t ti = (m0 + wm * WM + 16 * i) / 16, tj = (n0 + wn * WN + 16 * j) / 16;
+      if (ti < a.p_nti && tj < a.p_ntj)
+        *(reinterpret_cast<f32x4*>(a.part + ((split * a.p_nti + ti) * a.p_ntj + tj) * TILE) + l) = acc[i][j];
+    }
+}
+
+// out[row][col] = scale * sum_split part - corr * X[row + xoff][col]  (X row in range)
+__global__ __launch_bounds__(256) void k_nce_grad_finish(const float* __restrict__ part, int64_t n_split,
+                                                         int64_t p_nti, int64_t p_ntj, int64_t rows, int d,
+                                                         float scale, float corr, const float* __restrict__ X,
+                                                         int64_t x_rows, int64_t xoff, float* __restrict__ out) {
+  const int64_t tile_elems = p_nti * p_ntj * 64;  // float4 per split
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tile_elems;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 s = zero4();
+    for (int64_t sp = 0; sp < n_split; ++sp) s += reinterpret_cast<const f32x4*>(part)[sp * tile_elems + e];
+    const int64_t t = e >> 6;
+    const int ln = (int)(e & 63);
+    const int64_t ti = t / p_ntj, tj = t % p_ntj;
+    const int64_t col = tj * 16 + (ln & 15);
+    if (col >= d) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t row = ti * 16 + 4 * (ln >> 4) + q;
+      if (row >= rows) continue;
+      const int64_t xr = row + xoff;
+      const float xv = (xr >= 0 && xr < x_rows) ? X[xr * d + col] : 0.f;
+      out[row * d + col] = s[q] * scale - corr * xv;
+    }
+  }
+}
+
+// max squared row norms of F (m rows) and C (n rows) -> norm2[0], norm2[1]
+// (float bit patterns of non-negative values order like the values)
+__global__ __launch_bounds__(256) void k_nce_norms(const float* __restrict__ F, const float* __restrict__ C,
+                                                   int64_t m, int64_t n, int d, float* norm2) {
+  const int r = lane_id() & 15;
+  const int64_t groups = (int64_t)gridDim.x * 16;
+  float mf = 0.f, mc = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); row < m + n; row += groups) {
+    const float* p = row < m ? F + row * d : C + (row - m) * d;
+    float s = 0.f;
+    for (int k = r; k < d; k += 16) s += p[k] * p[k];
+    s = row_reduce16(s);
+    if (row < m) mf = fmaxf(mf, s); else mc = fmaxf(mc, s);
+  }
+  if (r == 0) {
+    atomicMax(reinterpret_cast<unsigned*>(norm2), __float_as_uint(mf));
+    atomicMax(reinterpret_cast<unsigned*>(norm2) + 1, __float_as_uint(mc));
+  }
+}
+
+__device__ __forceinline__ float nce_shift(const float* norm2, float inv_tau) {
+  return sqrtf(norm2[0]) * sqrtf(norm2[1]) * inv_tau;
+}
+
+__global__ __launch_bounds__(256) void k_nce_set_shift(const float* norm2, float inv_tau, float* shift) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *shift = nce_shift(norm2, inv_tau);
+}
+
+// fixed-order sums of the per-wave partials: rowsum[i] (i < m_pad), colsum[j] (j < n_pad)
+__global__ __launch_bounds__(256) void k_nce_sums(const float* __restrict__ rowpart, int64_t n_rp, int64_t m_pad,
+                                                  const float* __restrict__ colpart, int64_t n_cp, int64_t n_pad,
+                                                  float* __restrict__ rowsum, float* __restrict__ colsum) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m_pad + n_pad;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    if (e < m_pad) {
+      for (int64_t p = 0; p < n_rp; ++p) s += rowpart[p * m_pad + e];
+      rowsum[e] = s;
+    } else {
+      const int64_t j = e - m_pad;
+      for (int64_t p = 0; p < n_cp; ++p) s += colpart[p * n_pad + j];
+      colsum[j] = s;
+    }
+  }
+}
+
+// loss contribution of local rows i (row term) and columns j = row0 + i
+// (column term), plus the softmax scales a_i = 1/rowsum_i, b_j = 1/colsum_j
+// (zero in the padding).  loss += sum / (2 B).
+__global__ __launch_bounds__(256) void k_nce_loss(const float* __restrict__ rowsum, const float* __restrict__ colsum,
+                                                  const float* __restrict__ diag, int64_t m, int64_t m_pad,
+                                                  int64_t n, int64_t n_pad, int64_t row0, float inv_2b,
+                                                  const float* __restrict__ shift, float* __restrict__ a,
+                                                  float* __restrict__ b, float* loss, int* status) {
+  __shared__ float red[4];
+  const float sh = *shift;
+  float acc = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m_pad + n_pad;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    bool bad = false;
+    if (e < m_pad) {
+      a[e] = e < m ? 1.f / rowsum[e] : 0.f;
+      if (e < m) {
+        const float dg = diag[e];
+        acc += (logf(rowsum[e]) + sh - dg) + (logf(colsum[row0 + e]) + sh - dg);
+        bad = !(rowsum[e] >= SUM_MIN);
+      }
+    } else {
+      const int64_t j = e - m_pad;
+      b[j] = j < n ? 1.f / colsum[j] : 0.f;
+      bad = j < n && !(colsum[j] >= SUM_MIN);
+    }
+    if (bad && status) atomicAdd(status, 1);
+  }
+  acc = wave_reduce(acc);
+  if (lane_id() == 0) red[wave_id()] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss, (red[0] + red[1] + red[2] + red[3]) * inv_2b);
+}
+
+__global__ __launch_bounds__(256) void k_rank_finish(const int* __restrict__ cnt, int64_t m, int* __restrict__ rank) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x)
+    rank[e] = cnt[e] + 1;
+}
+
+}  // namespace nce
+}  // namespace tt

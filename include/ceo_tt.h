@@ -170,6 +170,49 @@ int32_t tt_cosine_mse_fwd_bwd(const float* u, const float* v, const float* targe
                               float* du, float* dv, float* loss_sum, float* dls_sum,
                               tt_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Contrastive scoring (BASELINE cfg 5).
+ *
+ * info_nce_loss (contrastive.py:102-138) over firm rows F [m, d] (a shard
+ * starting at global row row0) against ALL ceo rows C [n, d]:
+ *   S = F C^T / temperature,  loss = (CE(S, diag) + CE(S^T, diag)) / 2,
+ * with batch = the global B (n).  Data-parallel use: each rank passes its F
+ * shard and the all-gathered C; all-reduce MAX of norm2, SUM of col_sum and
+ * loss; the dc of every rank are summed (reduce-scatter) for the C shard.
+ *   1. tt_nce_norms    : norm2 = {max_i |f_i|^2, max_j |c_j|^2}; the shared
+ *      exponent shift sqrt(norm2[0] norm2[1]) / temperature bounds every
+ *      logit, so one exp per element serves both softmaxes.
+ *   2. tt_nce_forward  : E = exp(S - shift) kept in ws, row sums, diag;
+ *      col_sum[n] = column sums of E over these m rows.
+ *   3. tt_nce_loss     : loss += this shard's share (col_sum complete);
+ *      *status += number of row / column sums below 1e-30 (exp underflow,
+ *      inputs far from L2-normalised): the result is invalid if > 0.
+ *   4. tt_nce_backward : df [m, d] (complete), dc [n, d] (this shard's
+ *      contribution).  ws must hold the forward's E.
+ * ws: tt_nce_workspace_bytes(m, n, d) bytes (E alone is 4 m n bytes).     */
+int64_t tt_nce_workspace_bytes(int64_t m, int64_t n, int32_t d);
+int32_t tt_nce_norms(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                     float* norm2, tt_stream_t stream);
+int32_t tt_nce_forward(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                       int64_t row0, float temperature, const float* norm2, void* ws,
+                       int64_t ws_bytes, float* col_sum, tt_stream_t stream);
+int32_t tt_nce_loss(int64_t m, int64_t n, int32_t d, int64_t row0, int64_t batch,
+                    float temperature, void* ws, int64_t ws_bytes, const float* col_sum,
+                    float* loss, int32_t* status, tt_stream_t stream);
+int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                        int64_t row0, int64_t batch, float temperature, void* ws,
+                        int64_t ws_bytes, float* df, float* dc, tt_stream_t stream);
+
+/* compute_retrieval_metrics (contrastive.py:275-332): for firm rows F [m, d]
+ * (global rows row0..) against all n ceo rows C, ranks[i] = 1 + #{j != row0+i :
+ * f_i.c_j > f_i.c_{row0+i}} -- the rank of the true match under a descending
+ * sort (identical to torch.sort's whenever the row has no exact ties).
+ * ws: tt_rank_workspace_bytes(m) bytes.                                     */
+int64_t tt_rank_workspace_bytes(int64_t m);
+int32_t tt_retrieval_ranks(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                           int64_t row0, void* ws, int64_t ws_bytes, int32_t* ranks,
+                           tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

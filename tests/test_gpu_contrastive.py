@@ -1,0 +1,175 @@
+"""HIP contrastive kernels (tt_nce_*, tt_retrieval_ranks) vs the reference's
+golden vectors (tests/golden/contrastive.npz) and the CPU oracle
+(oracle/contrastive.py).  Tolerance: normwise 1e-5 (loss: relative 1e-5)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import load_golden, normwise
+from oracle import contrastive as OC
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _nce(f, c, tau=0.07):
+    from ceo_firm_matching.contrastive import info_nce_loss
+    f = f.clone().requires_grad_(True)
+    c = c.clone().requires_grad_(True)
+    loss = info_nce_loss(f, c, tau)
+    if loss.requires_grad:
+        loss.backward()
+    return loss, f.grad, c.grad
+
+
+@pytest.mark.parametrize("case", ["b1", "b2", "b64", "b256", "raw256"])
+def test_info_nce_golden(case):
+    dev = _dev()
+    g = load_golden("contrastive")
+    f = torch.from_numpy(g[f"nce/{case}/f"]).to(dev)
+    c = torch.from_numpy(g[f"nce/{case}/c"]).to(dev)
+    loss, df, dc = _nce(f, c)
+    ref = float(g[f"nce/{case}/loss64"])
+    assert abs(float(loss.detach()) - ref) <= TOL * max(1.0, abs(ref)), (float(loss.detach()), ref)
+    if f.shape[0] <= 1:
+        assert df is None
+        return
+    assert normwise(df.cpu().numpy(), g[f"nce/{case}/df64"]) < TOL
+    assert normwise(dc.cpu().numpy(), g[f"nce/{case}/dc64"]) < TOL
+
+
+@pytest.mark.parametrize("B,D", [(3000, 256), (1000, 100), (517, 36), (4100, 64)])
+def test_info_nce_ragged_vs_oracle(B, D):
+    """Partial tiles, several blocks / K splits, D not a multiple of 16."""
+    dev = _dev()
+    gen = torch.Generator().manual_seed(B + D)
+    f = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(B, D, generator=gen) + 0.3 * f, dim=1)
+    loss, df, dc = _nce(f.to(dev), c.to(dev))
+    rl, rdf, rdc = OC.info_nce(f.double(), c.double(), 0.07)
+    assert abs(float(loss) - float(rl)) <= TOL * abs(float(rl))
+    assert normwise(df.cpu().numpy(), rdf.numpy()) < TOL
+    assert normwise(dc.cpu().numpy(), rdc.numpy()) < TOL
+
+
+def test_info_nce_row_shards_compose():
+    """The sharded decomposition (row0 offsets, partial column sums, partial
+    dC) reproduces the full loss on one device -- the multi-GPU algebra."""
+    from ceo_firm_matching.contrastive import _NCE
+    dev = _dev()
+    gen = torch.Generator().manual_seed(3)
+    B, D, W = 2048, 128, 4
+    f = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1).to(dev)
+    c = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1).to(dev)
+    m = B // W
+    hs = [_NCE(f[r * m:(r + 1) * m].contiguous(), c, m, B, D, r * m, B, 0.07) for r in range(W)]
+    n2 = torch.stack([h.norms() for h in hs]).max(dim=0).values
+    col = sum(h.forward(n2) for h in hs)
+    parts = [h.loss(col) for h in hs]
+    assert sum(int(st.item()) for _, st in parts) == 0
+    loss = sum(lo for lo, _ in parts)
+    grads = [h.backward() for h in hs]
+    df = torch.cat([g_[0] for g_ in grads])
+    dc = sum(g_[1] for g_ in grads)
+    rl, rdf, rdc = OC.info_nce(f.cpu().double(), c.cpu().double(), 0.07)
+    assert abs(float(loss) - float(rl)) <= TOL * abs(float(rl))
+    assert normwise(df.cpu().numpy(), rdf.numpy()) < TOL
+    assert normwise(dc.cpu().numpy(), rdc.numpy()) < TOL
+
+
+def test_info_nce_rejects_underflowing_inputs():
+    """Far-from-normalised inputs whose softmax sums underflow the shared
+    exponent shift are reported, never returned as inf/nan."""
+    dev = _dev()
+    from ceo_firm_matching.contrastive import info_nce_loss
+    gen = torch.Generator().manual_seed(1)
+    f = torch.nn.functional.normalize(torch.randn(64, 32, generator=gen), dim=1)
+    f[0] *= 40.0  # one long row: shift = 40/tau, the other rows' sums underflow
+    with pytest.raises(NotImplementedError):
+        info_nce_loss(f.to(dev), f.to(dev).clone())
+
+
+def test_retrieval_golden_metrics():
+    dev = _dev()
+    from ceo_firm_matching.contrastive import metrics_from_ranks, retrieval_ranks
+    g = load_golden("contrastive")
+    fe = torch.from_numpy(g["ret/firm_emb"]).to(dev)
+    ce = torch.from_numpy(g["ret/ceo_emb"]).to(dev)
+    got = metrics_from_ranks(retrieval_ranks(fe, ce))
+    for k in ("recall@1", "recall@5", "recall@10", "MRR", "median_rank"):
+        assert got[k] == pytest.approx(float(g[f"ret/metric/{k}"]), rel=1e-12, abs=1e-12), k
+
+
+@pytest.mark.parametrize("N,D,cap", [(5000, 256, 5000), (7000, 64, None), (333, 30 + 2, None)])
+def test_retrieval_ranks_vs_oracle(N, D, cap):
+    dev = _dev()
+    from ceo_firm_matching.contrastive import retrieval_ranks
+    gen = torch.Generator().manual_seed(N)
+    f = torch.nn.functional.normalize(torch.randn(N, D, generator=gen), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(N, D, generator=gen) + 0.5 * f, dim=1)
+    got = retrieval_ranks(f.to(dev), c.to(dev), cap=cap).cpu().numpy()
+    ref = OC.retrieval_ranks(f, c, cap=cap)
+    # fp32 GEMM vs fp64: a pair may only swap order when the scores agree to fp32 rounding
+    bad = np.nonzero(got != ref)[0]
+    assert len(bad) <= max(1, len(ref) // 1000), bad[:10]
+    assert np.all(np.abs(got[bad] - ref[bad]) <= 1)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _sharded_rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching.contrastive import info_nce_loss_sharded
+        dev = torch.device("cuda:0")
+        gen = torch.Generator().manual_seed(9)
+        B, D = 1024, 64
+        f = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1)
+        c = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1)
+        m = B // world
+        fl = f[rank * m:(rank + 1) * m].to(dev).requires_grad_(True)
+        cl = c[rank * m:(rank + 1) * m].to(dev).requires_grad_(True)
+        loss = info_nce_loss_sharded(fl, cl, 0.07)
+        loss.backward()
+        rl, rdf, rdc = OC.info_nce(f.double(), c.double(), 0.07)
+        e = (abs(float(loss) - float(rl)) / abs(float(rl)),
+             normwise(fl.grad.cpu().numpy(), rdf[rank * m:(rank + 1) * m].numpy()),
+             normwise(cl.grad.cpu().numpy(), rdc[rank * m:(rank + 1) * m].numpy()))
+        q.put((rank, max(e)))
+    except Exception as ex:
+        q.put((rank, repr(ex)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_info_nce_sharded_two_ranks():
+    _dev()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sharded_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=120)
+    for rank, err in res:
+        assert isinstance(err, float) and err < TOL, (rank, err)

@@ -174,6 +174,80 @@ def cosine_roofline(dev, D=128, n=1 << 22, reps=20):
             "frac_of_measured_stream": round(gbs / stream, 4), "pairs_per_s": round(n / (ms * 1e-3), 1)}
 
 
+def contrastive_cpu(D=256, B=4096):
+    """CPU oracle InfoNCE fwd+bwd (the reference's info_nce_loss algebra) at
+    B=4096, extrapolated to N x N pairs (work grows as B^2)."""
+    from oracle import contrastive as OC
+    g = torch.Generator().manual_seed(0)
+    f = torch.nn.functional.normalize(torch.randn(B, D, generator=g), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(B, D, generator=g), dim=1)
+    OC.info_nce(f, c, 0.07)
+    t0 = time.perf_counter()
+    OC.info_nce(f, c, 0.07)
+    t = time.perf_counter() - t0
+    return {"sample": f"oracle info_nce fwd+bwd at B={B}, D={D}, fp32, {torch.get_num_threads()} threads",
+            "seconds": round(t, 4), "scored_pairs_per_s": round(B * B / t, 1), "kind": "port",
+            "cores": torch.get_num_threads()}
+
+
+def contrastive_leg(dev, pg, world, rank, N=100_000, D=256, reps=3, cpu=False):
+    """BASELINE cfg 5: symmetric InfoNCE fwd+bwd over the full N x N scoring
+    matrix (N firms x N CEOs, D=256, L2-normalised synthetic embeddings),
+    pairs sharded over the ranks (RCCL all-gather / all-reduce /
+    reduce-scatter), plus retrieval ranks of every firm among all N CEOs."""
+    from ceo_firm_matching.contrastive import info_nce_loss, info_nce_loss_sharded, retrieval_ranks_rows
+    m = N // world
+    g = torch.Generator(device=dev).manual_seed(500 + rank)
+    f = torch.nn.functional.normalize(torch.randn(m, D, device=dev, generator=g), dim=1).requires_grad_(True)
+    c = torch.nn.functional.normalize(torch.randn(m, D, device=dev, generator=g), dim=1).requires_grad_(True)
+
+    def step():
+        f.grad = None
+        c.grad = None
+        loss = info_nce_loss_sharded(f, c, 0.07, group=pg) if pg is not None else info_nce_loss(f, c, 0.07)
+        loss.backward()
+        return loss
+
+    step()
+    torch.cuda.synchronize()
+    if pg is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        loss = step()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    # retrieval ranks of this rank's firms against all CEOs
+    with torch.no_grad():
+        if pg is not None:
+            c_all = torch.empty(N, D, device=dev)
+            dist.all_gather_into_tensor(c_all, c.detach())
+        else:
+            c_all = c.detach()
+        retrieval_ranks_rows(f.detach(), c_all, rank * m)
+        torch.cuda.synchronize()
+        if pg is not None:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            ranks = retrieval_ranks_rows(f.detach(), c_all, rank * m)
+        torch.cuda.synchronize()
+        tr = (time.perf_counter() - t1) / reps
+    if pg is not None:
+        tt = torch.tensor([t, tr], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t, tr = tt.tolist()
+    flops = 3 * 2.0 * N * N * D  # S, dF, dC GEMMs
+    return {"workload": f"cfg5: InfoNCE fwd+bwd, {N} firms x {N} CEOs, D={D}, tau=0.07, fp32, "
+                        f"pairs sharded over {world} GPU(s)",
+            "ms_per_step": round(t * 1e3, 3), "scored_pairs_per_s": round(N * N / t, 1),
+            "achieved_tflops": round(flops / t / 1e12, 2), "peak_tflops": round(PEAK_FP32_TFLOPS * world, 1),
+            "frac": round(flops / t / 1e12 / (PEAK_FP32_TFLOPS * world), 4), "bound": "mfma",
+            "loss": round(float(loss.detach()), 6),
+            "retrieval_ranks_ms": round(tr * 1e3, 3), "ranks_median": float(ranks.float().median()),
+            "cpu_baseline": contrastive_cpu(D) if cpu else None}
+
+
 def _guard_stdout():
     """Route everything native libraries print to stdout (RCCL prints its
     version banner there at communicator init) to stderr, and return a
@@ -344,6 +418,12 @@ def main():
         result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)
         if rank == 0:
             result["cosine_roofline"] = cosine_roofline(dev, D=D)
+        # drop the training state before the 40 GB (N=1) similarity workspace
+        del tr, model, data, rows
+        graph = None
+        torch.cuda.empty_cache()
+        result["contrastive"] = contrastive_leg(dev, pg, world, rank,
+                                                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(nf, nc, D, B)

@@ -171,3 +171,40 @@ def test_product_path_refuses_without_extension(monkeypatch):
     monkeypatch.setattr(N, "LIB_PATH", os.path.join(ROOT, "does-not-exist", "libceo_tt.so"))
     with pytest.raises(N.NativeLibraryError, match="HIP extension not built"):
         N.lib()
+
+
+def test_contrastive_host_argument_errors():
+    L = N.lib()
+    buf = _fake()
+    p = buf.ctypes.data
+    assert L.tt_nce_workspace_bytes(0, 10, 16) == N.TT_ERR_ARG
+    assert L.tt_nce_workspace_bytes(10, 10, 6) == N.TT_ERR_ARG  # d % 4
+    ws = L.tt_nce_workspace_bytes(100, 100, 32)
+    assert ws >= 4 * 100 * 100
+    # 100k x 100k at D=256: E (40 GB) dominates; fits one MI355X (288 GB)
+    big = L.tt_nce_workspace_bytes(100_000, 100_000, 256)
+    assert 4 * 100_000 ** 2 <= big < 45 * 2 ** 30
+    # row shard outside the CEO range / short workspace / bad temperature
+    assert L.tt_nce_forward(p, p, 60, 100, 32, 50, ctypes.c_float(0.07), p, p, ws, p, None) == N.TT_ERR_ARG
+    assert L.tt_nce_forward(p, p, 100, 100, 32, 0, ctypes.c_float(0.07), p, p, ws - 4, p, None) == N.TT_ERR_WORKSPACE
+    assert L.tt_nce_forward(p, p, 100, 100, 32, 0, ctypes.c_float(0.0), p, p, ws, p, None) == N.TT_ERR_ARG
+    assert L.tt_nce_loss(100, 100, 32, 0, 1, ctypes.c_float(0.07), p, ws, p, p, None, None) == N.TT_ERR_ARG
+    assert L.tt_nce_backward(p, None, 100, 100, 32, 0, 100, ctypes.c_float(0.07), p, ws, p, p, None) == N.TT_ERR_ARG
+    assert L.tt_rank_workspace_bytes(0) == N.TT_ERR_ARG
+    rb = L.tt_rank_workspace_bytes(100)
+    assert L.tt_retrieval_ranks(p, p, 100, 100, 32, 0, p, rb - 4, p, None) == N.TT_ERR_WORKSPACE
+
+
+def test_contrastive_cpu_path_matches_oracle():
+    """CPU tensors evaluate the reference expression (no HIP device)."""
+    from oracle import contrastive as OC
+    from ceo_firm_matching.contrastive import info_nce_loss, metrics_from_ranks, retrieval_ranks
+    g = load_golden("contrastive")
+    f = torch.from_numpy(g["nce/b64/f"])
+    c = torch.from_numpy(g["nce/b64/c"])
+    assert abs(float(info_nce_loss(f, c)) - float(g["nce/b64/loss"])) < 1e-5
+    assert float(info_nce_loss(f[:1], c[:1])) == 0.0
+    fe = torch.from_numpy(g["ret/firm_emb"])
+    ce = torch.from_numpy(g["ret/ceo_emb"])
+    got = metrics_from_ranks(retrieval_ranks(fe, ce))
+    assert got == OC.retrieval_metrics(OC.retrieval_ranks(fe, ce))

@@ -91,7 +91,7 @@ static Layout make_layout(const tt_model_desc* d) {
 }
 
 struct WsLayout {
-  int64_t Z0[2], Z4[2], dY0[2], dY1[2], st0[2], st1[2], sh0[2], sh1[2], fin0[2], fin1[2];
+  int64_t Z0[2], Z4[2], dY0[2], dY1[2], st0[2], st1[2], sh0[2], sh1[2], fin0[2], fin1[2], bng[2], lsr;
   int64_t tgw;
   int64_t slab[2];
   int64_t gacc;
@@ -113,13 +113,15 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
   int64_t off = 0;
   auto take = [&](int64_t n) { const int64_t o = off; off += round_up(n, 64); return o; };
   for (int t = 0; t < 2; ++t) {
-    W.st0[t] = take(2 * H0);
-    W.st1[t] = take(2 * H1);
+    W.st0[t] = take(NREP * 2 * H0);
+    W.st1[t] = take(NREP * 2 * H1);
+    W.bng[t] = take(NREP * BNG);
     W.sh0[t] = take(H0);
     W.sh1[t] = take(H1);
     W.fin0[t] = take(2 * H0);
     W.fin1[t] = take(2 * H1);
   }
+  W.lsr = take(NREP * LSR);
   W.gacc = take(L.n);
   const int64_t rows = padded_rows(max_batch);
   W.n_tiles = (int)(rows / ROWS);
@@ -236,10 +238,11 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
       T.nbt0 = nbt + 2 * t;
       T.nbt1 = nbt + 2 * t + 1;
     }
-    T.gg0 = gacc + s[TT_SLOT_G0];
-    T.gbe0 = gacc + s[TT_SLOT_BE0];
-    T.gg1 = gacc + s[TT_SLOT_G1];
-    T.gbe1 = gacc + s[TT_SLOT_BE1];
+    float* bng = ws + W.bng[t];
+    T.gg0 = bng;
+    T.gbe0 = bng + H0;
+    T.gg1 = bng + 2 * H0;
+    T.gbe1 = bng + 2 * H0 + H1;
     T.Z0 = ws + W.Z0[t];
     T.Z4 = ws + W.Z4[t];
     T.dY0 = ws + W.dY0[t];
@@ -274,7 +277,7 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.n_tiles = (int)((b->n_rows + ROWS - 1) / ROWS);
   a.slab_ld = (int)L.slab_ld;
   a.logit_scale = params + L.ls;
-  a.g_ls = ws + W.gacc + L.ls;
+  a.lsr = ws + W.lsr;
   a.tgw = ws + W.tgw;
 }
 
@@ -286,7 +289,8 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   RedArgs r;
   std::memset(&r, 0, sizeof(r));
   int k = 0;
-  auto add = [&](int64_t off, int64_t len, int kind, int tower, int64_t so, int n_slabs) {
+  auto add = [&](int64_t off, int64_t len, int kind, int tower, int64_t so, int n_slabs, float* rep = nullptr,
+                 int64_t rep_stride = 0) {
     if (len <= 0) return;
     r.seg[k].off = off;
     r.seg[k].len = len;
@@ -294,19 +298,24 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     r.seg[k].tower = tower;
     r.seg[k].slab_off = so;
     r.seg[k].n_slabs = n_slabs;
+    r.seg[k].rep = rep;
+    r.seg[k].rep_stride = rep_stride;
     ++k;
   };
   int64_t emb_total = L.slot[0][TT_SLOT_W0];
   add(0, emb_total, 1, 0, 0, 0);
   for (int t = 0; t < 2; ++t) {
     const int64_t* s = L.slot[t];
+    float* bng = ws + W.bng[t];
+    // gamma|beta slots are adjacent and unpadded (H0, H1 multiples of 4): same order as a replica
     add(s[TT_SLOT_W0], s[TT_SLOT_G0] - s[TT_SLOT_W0], 0, t, L.so[t][0], P.n_tiles);
-    add(s[TT_SLOT_G0], s[TT_SLOT_W4] - s[TT_SLOT_G0], 1, t, 0, 0);
+    add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, bng, BNG);
     add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles);
-    add(s[TT_SLOT_G1], s[TT_SLOT_W8] - s[TT_SLOT_G1], 1, t, 0, 0);
+    add(s[TT_SLOT_G1], 2 * H1, 2, t, 0, 0, bng + 2 * H0, BNG);
     add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], 0, t, L.so[t][4], P.n_tiles_top);
   }
-  add(L.ls, 1, 1, 0, 0, 0);
+  add(L.ls, 1, 2, 0, 0, 0, ws + W.lsr, LSR);
+  r.lsr = ws + W.lsr;
   r.n_seg = k;
   r.n_slabs = P.n_tiles;
   r.n = L.n;
@@ -436,8 +445,8 @@ int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, 
   a.score = score;
   if (train) {
     for (int t = 0; t < 2; ++t) {
-      (void)hipMemsetAsync(w + c.W.st0[t], 0, sizeof(float) * 2 * H0, s);
-      (void)hipMemsetAsync(w + c.W.st1[t], 0, sizeof(float) * 2 * H1, s);
+      (void)hipMemsetAsync(w + c.W.st0[t], 0, sizeof(float) * NREP * 2 * H0, s);
+      (void)hipMemsetAsync(w + c.W.st1[t], 0, sizeof(float) * NREP * 2 * H1, s);
     }
   }
   launch_l0(a, c.P, s);
@@ -464,6 +473,8 @@ int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch*
   a.mode = TOP_BWD_GIVEN;
   a.dscore = dscore;
   (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
+  for (int t = 0; t < 2; ++t) (void)hipMemsetAsync(w + c.W.bng[t], 0, sizeof(float) * NREP * BNG, s);
+  (void)hipMemsetAsync(w + c.W.lsr, 0, sizeof(float) * NREP * LSR, s);
   launch_top(a, c.P, 2, s);
   launch_mid(a, c.P, s);
   launch_first(a, c.P, s);
@@ -492,7 +503,6 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   a.seed = seed;
   a.state = state;
   a.mode = TOP_TRAIN;
-  a.loss_sum = &state->loss_sum;
   auto ev = [&](int k) {
     Evs e;
     if (events) {
@@ -509,10 +519,11 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   for (int t = 0; t < 2; ++t) {
     r.zero_buf[2 * t] = w + c.W.st0[t];
-    r.zero_len[2 * t] = 2 * H0;
+    r.zero_len[2 * t] = NREP * 2 * H0;
     r.zero_buf[2 * t + 1] = w + c.W.st1[t];
-    r.zero_len[2 * t + 1] = 2 * H1;
+    r.zero_len[2 * t + 1] = NREP * 2 * H1;
   }
+  r.loss_state = state;
   if (apply_adam) {
     r.apply_adam = 1;
     r.p = params;

@@ -18,6 +18,15 @@ constexpr int WAVES = ROWS / 16;
 constexpr int THREADS = WAVES * WAVE;
 constexpr int TOP_ROWS_MAX = 128;  // k_top may use 128-row tiles (8 waves)
 constexpr int MAX_KP = 256;  // padded tower input width supported by the fused kernels
+// Cross-block sums (BN moments, BN-affine grads, logit-scale grad, loss) are
+// accumulated into NREP replicas picked by blockIdx.x: 512 blocks adding into
+// the same 128 addresses serialise at the memory-side atomic unit (measured:
+// +4.5 us on k_l0_fwd); with replicas each address sees 1/NREP of the adds and
+// the consumers sum NREP values.
+constexpr int NREP = 16;
+constexpr int BNG = 2 * H0 + 2 * H1;  // one replica of a tower's BN-affine grads: gg0|gbe0|gg1|gbe1
+constexpr int LSR = 32;               // replica stride of the (dls, loss) pair
+__device__ __forceinline__ int rep_of_block() { return (int)(blockIdx.x % NREP); }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -168,10 +177,10 @@ struct TowerDev {
   const float *W0, *b0, *g0, *be0, *W4, *b4, *g1, *be1, *W8, *b8;
   float *rm0, *rv0, *rm1, *rv1;           // BN running stats
   int64_t *nbt0, *nbt1;                   // num_batches_tracked
-  float *gg0, *gbe0, *gg1, *gbe1;         // BN affine grad accumulators (gacc arena)
+  float *gg0, *gbe0, *gg1, *gbe1;         // BN affine grad accumulators: replica r at +r*BNG
   // workspace
   float *Z0, *Z4, *dY0, *dY1;             // [B,64] [B,32] [B,64] [B,32]
-  float *st0, *st1;                       // shifted moment sums S1|S2 [2*64], [2*32]
+  float *st0, *st1;                       // shifted moment sums S1|S2 [NREP][2*64], [NREP][2*32]
   float *shift0, *shift1;                 // shifts used for S1/S2 [64], [32]
   float *fin0, *fin1;                     // finalized mean|invstd [2*64], [2*32]
   float* slab;                            // [n_slabs][slab_ld] partial dW/db sums
@@ -200,10 +209,9 @@ struct StepArgs {
   int D, n_tiles, slab_ld;
   int mode;              // TopMode for the top kernel
   const float* logit_scale;
-  float* g_ls;           // gacc slot of logit_scale
+  float* lsr;            // [NREP][LSR] replicas: [0] dL/dlogit_scale, [1] batch-mean loss
   float* score;          // [B] output scores (nullable)
   const float* dscore;   // [B] upstream grad (TOP_BWD_GIVEN)
-  float* loss_sum;       // [1] += sum w (s-t)^2 / B   (TOP_TRAIN)
   float* tgw;            // [Bpad][2] (target, weight) of each batch row, gathered by k_l0_fwd
 };
 
@@ -408,8 +416,10 @@ constexpr int RED_G = 8;    // slab groups per element
 struct Seg {
   int64_t off, len;      // range in the parameter arena
   int64_t slab_off;      // offset of the range inside a tower slab (kind 0)
-  int32_t kind, tower;   // kind 0: slab partials, 1: atomic accumulator (gacc)
+  int32_t kind, tower;   // kind 0: slab partials, 1: atomic accumulator (gacc), 2: NREP replicas
   int32_t n_slabs, pad;  // partial slabs to sum (kind 0)
+  float* rep;            // kind 2: replica 0 of the range; replica r at + r * rep_stride
+  int64_t rep_stride;
 };
 
 struct RedArgs {
@@ -423,6 +433,8 @@ struct RedArgs {
   float* grad;
   float* zero_buf[4];
   int32_t zero_len[4];
+  float* lsr;            // (dls, loss) replicas: loss folded into state->loss_sum
+  tt_state* loss_state;
   int32_t apply_adam;
   float* p; float* m; float* v;
   float lr, b1, b2, eps;

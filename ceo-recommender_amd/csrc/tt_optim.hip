@@ -66,15 +66,31 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
 #pragma unroll
         for (int k = 0; k < UNR; ++k) acc += (p0 + k * RED_G < n) ? v[k] : 0.f;
       }
-    } else if (pg == 0) {
-      acc = a.gacc[e];
+    } else if (S.kind == 1) {
+      if (pg == 0) acc = a.gacc[e];
+    } else {  // replicas: group pg sums replicas pg, pg + RED_G, ... (fixed order) and zeroes them
+      float* rp = S.rep + (e - S.off);
+#pragma unroll
+      for (int q = pg; q < NREP; q += RED_G) {
+        acc += rp[q * S.rep_stride];
+        rp[q * S.rep_stride] = 0.f;
+      }
     }
   }
   part[pg][el] = acc;
-  // zero the BN moment sums consumed by this step (one block)
-  if (blockIdx.x == 0)
+  // zero the BN moment sums consumed by this step; fold the loss replicas (one block)
+  if (blockIdx.x == 0) {
     for (int b = 0; b < 4; ++b)
       for (int i = threadIdx.x; i < a.zero_len[b]; i += blockDim.x) a.zero_buf[b][i] = 0.f;
+    if (a.lsr && threadIdx.x == 0) {
+      float l = 0.f;
+      for (int q = 0; q < NREP; ++q) {
+        l += a.lsr[q * LSR + 1];
+        a.lsr[q * LSR + 1] = 0.f;
+      }
+      if (a.loss_state) a.loss_state->loss_sum += l;
+    }
+  }
   __syncthreads();
   TT_STAMP(5, 1);
   if (pg != 0 || si < 0) return;

@@ -49,8 +49,14 @@ __device__ __forceinline__ void bn_coefs(const StepArgs& a, int H, const float* 
   float mean, var;
   if (a.train) {
     const double Bd = (double)a.B;
-    const float m1 = st[c] / (float)Bd;
-    var = st[H + c] / (float)Bd - m1 * m1;
+    float s1 = 0.f, s2 = 0.f;  // sum the NREP replicas (fixed order)
+#pragma unroll
+    for (int q = 0; q < NREP; ++q) {
+      s1 += st[q * 2 * H + c];
+      s2 += st[q * 2 * H + H + c];
+    }
+    const float m1 = s1 / (float)Bd;
+    var = s2 / (float)Bd - m1 * m1;
     var = var < 0.f ? 0.f : var;
     mean = shift[c] + m1;
     if (update) {
@@ -288,7 +294,7 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
     for (int i = 0; i < 4; ++i) T.Z0[(r0 + 16 * w + 4 * g + i) * H0 + 16 * j + r] = acc[j][i];
   if (a.train) {
     __syncthreads();
-    if (threadIdx.x < 2 * H0) atomicAdd(&T.st0[threadIdx.x], red[threadIdx.x]);
+    if (threadIdx.x < 2 * H0) atomicAdd(&T.st0[rep_of_block() * 2 * H0 + threadIdx.x], red[threadIdx.x]);
   }
   TT_STAMP(0, 4);
 }
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
     for (int i = 0; i < 4; ++i) T.Z4[(r0 + 16 * w + 4 * g + i) * H1 + 16 * j + r] = acc[j][i];
   if (a.train) {
     __syncthreads();
-    if (threadIdx.x < 2 * H1) atomicAdd(&T.st1[threadIdx.x], red[threadIdx.x]);
+    if (threadIdx.x < 2 * H1) atomicAdd(&T.st1[rep_of_block() * 2 * H1 + threadIdx.x], red[threadIdx.x]);
   }
   TT_STAMP(1, 4);
 }
@@ -692,12 +698,13 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   TT_STAMP(2, 6);
 
   if (threadIdx.x < H1) {
-    atomicAdd(&T.gg1[threadIdx.x], smem[L::red + threadIdx.x]);
-    atomicAdd(&T.gbe1[threadIdx.x], smem[L::red + H1 + threadIdx.x]);
+    atomicAdd(&T.gg1[rep_of_block() * BNG + threadIdx.x], smem[L::red + threadIdx.x]);
+    atomicAdd(&T.gbe1[rep_of_block() * BNG + threadIdx.x], smem[L::red + H1 + threadIdx.x]);
   }
   if (own == 0 && threadIdx.x == 0) {
-    atomicAdd(a.g_ls, smem[L::scal + 1]);
-    if (a.mode == TOP_TRAIN && a.loss_sum) atomicAdd(a.loss_sum, smem[L::scal + 0] / (float)a.B);
+    float* lr = a.lsr + rep_of_block() * LSR;
+    atomicAdd(lr, smem[L::scal + 1]);
+    if (a.mode == TOP_TRAIN) atomicAdd(lr + 1, smem[L::scal + 0] / (float)a.B);
   }
   if (threadIdx.x < D) slab[T.so_b8 + threadIdx.x] = smem[L::db8 + threadIdx.x];
   TT_STAMP(2, 7);
@@ -752,8 +759,14 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     const int c = threadIdx.x;
     const float inv = T.fin1[H1 + c];
     c1[c] = inv * T.g1[c];
-    c1[H1 + c] = T.gbe1[c] * invB;
-    c1[2 * H1 + c] = T.gg1[c] * invB;
+    float sb = 0.f, sg = 0.f;
+#pragma unroll
+    for (int q = 0; q < NREP; ++q) {
+      sb += T.gbe1[q * BNG + c];
+      sg += T.gg1[q * BNG + c];
+    }
+    c1[H1 + c] = sb * invB;
+    c1[2 * H1 + c] = sg * invB;
     c1[3 * H1 + c] = T.fin1[c];
     c1[4 * H1 + c] = inv;
   } else if (threadIdx.x < H1 + H0) {
@@ -844,8 +857,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   __syncthreads();
   TT_STAMP(3, 3);
   if (threadIdx.x < H0) {
-    atomicAdd(&T.gg0[threadIdx.x], red[threadIdx.x]);
-    atomicAdd(&T.gbe0[threadIdx.x], red[H0 + threadIdx.x]);
+    atomicAdd(&T.gg0[rep_of_block() * BNG + threadIdx.x], red[threadIdx.x]);
+    atomicAdd(&T.gbe0[rep_of_block() * BNG + threadIdx.x], red[H0 + threadIdx.x]);
   }
   if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = db4[threadIdx.x];
   TT_STAMP(3, 4);
@@ -904,8 +917,14 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     const int c = threadIdx.x;
     const float inv = T.fin0[H0 + c];
     c0[c] = inv * T.g0[c];
-    c0[H0 + c] = T.gbe0[c] * invB;
-    c0[2 * H0 + c] = T.gg0[c] * invB;
+    float sb = 0.f, sg = 0.f;
+#pragma unroll
+    for (int q = 0; q < NREP; ++q) {
+      sb += T.gbe0[q * BNG + c];
+      sg += T.gg0[q * BNG + c];
+    }
+    c0[H0 + c] = sb * invB;
+    c0[2 * H0 + c] = sg * invB;
     c0[3 * H0 + c] = T.fin0[c];
     c0[4 * H0 + c] = inv;
     db0[c] = 0.f;

@@ -49,14 +49,8 @@ __device__ __forceinline__ void bn_coefs(const StepArgs& a, int H, const float* 
   float mean, var;
   if (a.train) {
     const double Bd = (double)a.B;
-    float s1 = 0.f, s2 = 0.f;  // sum the NREP replicas (fixed order)
-#pragma unroll
-    for (int q = 0; q < NREP; ++q) {
-      s1 += st[q * 2 * H + c];
-      s2 += st[q * 2 * H + H + c];
-    }
-    const float m1 = s1 / (float)Bd;
-    var = s2 / (float)Bd - m1 * m1;
+    const float m1 = st[c] / (float)Bd;  // st: replica-summed S1|S2 (LDS)
+    var = st[H + c] / (float)Bd - m1 * m1;
     var = var < 0.f ? 0.f : var;
     mean = shift[c] + m1;
     if (update) {
@@ -82,6 +76,36 @@ __device__ __forceinline__ float bn_relu_drop(float z, float mean, float alpha, 
   y = y > 0.f ? y : 0.f;
   if (drop) y = dropout_keep(key, ctr, thr) ? y * scale : 0.f;
   return y;
+}
+
+// Sum the NREP replicas of N consecutive cross-block accumulators (replica
+// stride `stride`) into dst[N] (LDS) with the whole block: every thread issues
+// its NREP/G loads at once (G = groups of N threads), fixed summation order.
+// Ends with dst visible to the block.  scratch: NTH floats of LDS.
+template <int NTH, int N>
+__device__ __forceinline__ void rep_sum(const float* rep, int stride, float* scratch, float* dst) {
+  constexpr int G0 = NTH / N;
+  constexpr int G = G0 < NREP ? G0 : NREP;
+  constexpr int PER = NREP / G;
+  static_assert(NTH % N == 0 && NREP % G == 0, "replica groups");
+  const int c = (int)threadIdx.x % N, grp = (int)threadIdx.x / N;
+  if (grp < G) {
+    float v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = rep[(grp + k * G) * stride + c];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) sum += v[k];
+    scratch[grp * N + c] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < G; ++q) sum += scratch[q * N + threadIdx.x];
+    dst[threadIdx.x] = sum;
+  }
+  __syncthreads();
 }
 
 // Block-wide column sums of NT C-layout tiles into LDS `red` (ds_add_f32).
@@ -306,7 +330,7 @@ template <int R>
 struct L4Lds {
   static constexpr int LD = H0 + 4;
   static constexpr size_t bytes =
-      sizeof(float) * ((size_t)(H1 + R) * LD + 3 * H0 + 2 * H1 + H0 + H1 + 4 * H1);
+      sizeof(float) * ((size_t)(H1 + R) * LD + 3 * H0 + 2 * H1 + H0 + H1 + 4 * H1 + 4 * R + 2 * H0);
 };
 
 template <int R>
@@ -327,6 +351,8 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
   float* a0r = red + 2 * H1;       // [64] A0 of batch row 0
   float* shl = a0r + H0;           // [32] moment shift = Z4 of batch row 0
   float* part = shl + H1;          // [4][32]
+  float* rsc = part + 4 * H1;      // [NTH] replica-sum scratch
+  float* rst = rsc + NTH;          // [2*64] BN0 moment sums S1|S2
   TT_STAMP(1, 0);
 
   // issue every load of the phase first (Z0 rows are padded: no clamp needed)
@@ -341,10 +367,11 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias[j] = T.b4[16 * j + r];
   const float z0r = threadIdx.x < H0 ? T.Z0[threadIdx.x] : 0.f;
+  if (a.train) rep_sum<NTH, 2 * H0>(T.st0, 2 * H0, rsc, rst);
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
     float mean, inv;
-    bn_coefs(a, H0, T.st0, T.shift0, T.rm0, T.rv0, T.nbt0, T.fin0, a.update_stats && blockIdx.x == 0, c, &mean,
+    bn_coefs(a, H0, rst, T.shift0, T.rm0, T.rv0, T.nbt0, T.fin0, a.update_stats && blockIdx.x == 0, c, &mean,
              &inv);
     cf[c] = mean;
     cf[H0 + c] = inv * T.g0[c];
@@ -434,7 +461,9 @@ struct TopLds {
   static constexpr int cf1 = db8 + DP;
   static constexpr int red = cf1 + 2 * 4 * H1;
   static constexpr int scal = red + 2 * H1;  // [0] loss part [1] dls part
-  static constexpr int total = scal + 4;
+  static constexpr int rsc = scal + 4;        // [4R] replica-sum scratch
+  static constexpr int rst = rsc + 4 * R;     // [2][2*32] BN1 moment sums S1|S2 per tower
+  static constexpr int total = rst + 4 * H1;
 };
 
 template <int NDT, int R>
@@ -494,12 +523,16 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
       tg[i] = a.dscore[min(row, a.B - 1)];
     }
   }
+  if (a.train) {
+    rep_sum<NTH, 2 * H1>(a.tw[0].st1, 2 * H1, smem + L::rsc, smem + L::rst);
+    rep_sum<NTH, 2 * H1>(a.tw[1].st1, 2 * H1, smem + L::rsc, smem + L::rst + 2 * H1);
+  }
   if (threadIdx.x < 2 * H1) {
     const int tau = threadIdx.x / H1, c = threadIdx.x % H1;
     const TowerDev& T = a.tw[tau];
     const bool upd = a.update_stats && blockIdx.x == 0 && (bwd ? tau == own : true);
     float mean, inv;
-    bn_coefs(a, H1, T.st1, T.shift1, T.rm1, T.rv1, T.nbt1, T.fin1, upd, c, &mean, &inv);
+    bn_coefs(a, H1, smem + L::rst + tau * 2 * H1, T.shift1, T.rm1, T.rv1, T.nbt1, T.fin1, upd, c, &mean, &inv);
     float* cf = smem + L::cf1 + tau * 4 * H1;
     cf[c] = mean;
     cf[H1 + c] = inv * T.g1[c];
@@ -718,7 +751,8 @@ struct MidLds {
   static constexpr int LDW = H0 + 4;   // W4 row-major [32][68]
   static constexpr int LDT = R + 4;    // transposed images [col][row]
   static constexpr size_t bytes =
-      sizeof(float) * ((size_t)H1 * LDW + (size_t)(H1 + H0) * LDT + H1 + 5 * H1 + 4 * H0 + 2 * H0);
+      sizeof(float) * ((size_t)H1 * LDW + (size_t)(H1 + H0) * LDT + H1 + 5 * H1 + 4 * H0 + 2 * H0 + 4 * R +
+                       2 * H1);
 };
 
 template <int R>
@@ -739,6 +773,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   float* c1 = db4 + H1;               // k1[32] mb[32] mg[32] mean1[32] inv1[32]
   float* c0 = c1 + 5 * H1;            // mean0[64] alpha0[64] beta0[64] inv0[64]
   float* red = c0 + 4 * H0;           // [128]
+  float* rsc = red + 2 * H0;          // [NTH] replica-sum scratch
+  float* rst = rsc + NTH;             // [2*32] sum dgamma1 | sum dbeta1
   TT_STAMP(3, 0);
 
   // issue the phase's loads: dY1, Z4 (2 tiles), Z0 (4 tiles) in C layout
@@ -755,18 +791,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     for (int j = 0; j < 4; ++j) zz0[j][i] = T.Z0[row * H0 + 16 * j + r];
   }
   const float invB = 1.f / (float)a.B;
+  rep_sum<NTH, 2 * H1>(T.gg1, BNG, rsc, rst);  // gg1|gbe1 are adjacent in a replica
   if (threadIdx.x < H1) {
     const int c = threadIdx.x;
     const float inv = T.fin1[H1 + c];
     c1[c] = inv * T.g1[c];
-    float sb = 0.f, sg = 0.f;
-#pragma unroll
-    for (int q = 0; q < NREP; ++q) {
-      sb += T.gbe1[q * BNG + c];
-      sg += T.gg1[q * BNG + c];
-    }
-    c1[H1 + c] = sb * invB;
-    c1[2 * H1 + c] = sg * invB;
+    c1[H1 + c] = rst[H1 + c] * invB;
+    c1[2 * H1 + c] = rst[c] * invB;
     c1[3 * H1 + c] = T.fin1[c];
     c1[4 * H1 + c] = inv;
   } else if (threadIdx.x < H1 + H0) {
@@ -876,7 +907,7 @@ struct FirstLds {
     return a > b ? a : b;
   }
   static size_t bytes(int kp) {
-    return sizeof(float) * (xt_floats(kp) + (size_t)H0 * LDT + H0 + 5 * H0 + 2 * R);
+    return sizeof(float) * (xt_floats(kp) + (size_t)H0 * LDT + H0 + 5 * H0 + 2 * R + 4 * R + 2 * H0);
   }
 };
 
@@ -899,6 +930,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   float* dZT = XT + FirstLds<R>::xt_floats(kp);        // [64][R+4]
   float* db0 = dZT + H0 * LDT;                         // [64]
   float* c0 = db0 + H0;                                // k0[64] mb[64] mg[64] mean0[64] inv0[64]
+  float* rsc = c0 + 5 * H0;                            // [NTH] replica-sum scratch
+  float* rst = rsc + NTH;                              // [2*64] sum dgamma0 | sum dbeta0
   TT_STAMP(4, 0);
 
   f32x4 dy0[4], zz0[4];
@@ -913,18 +946,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   }
   stage_ridx<R>(a, base, r0, ridx);
   const float invB = 1.f / (float)a.B;
+  rep_sum<NTH, 2 * H0>(T.gg0, BNG, rsc, rst);  // gg0|gbe0 are adjacent in a replica
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
     const float inv = T.fin0[H0 + c];
     c0[c] = inv * T.g0[c];
-    float sb = 0.f, sg = 0.f;
-#pragma unroll
-    for (int q = 0; q < NREP; ++q) {
-      sb += T.gbe0[q * BNG + c];
-      sg += T.gg0[q * BNG + c];
-    }
-    c0[H0 + c] = sb * invB;
-    c0[2 * H0 + c] = sg * invB;
+    c0[H0 + c] = rst[H0 + c] * invB;
+    c0[2 * H0 + c] = rst[c] * invB;
     c0[3 * H0 + c] = T.fin0[c];
     c0[4 * H0 + c] = inv;
     db0[c] = 0.f;

@@ -35,7 +35,7 @@ def main():
     L.tt_debug_set_stamps.argtypes = [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
     n_total, nf, nc, D, B = CONFIGS[cfgname]
-    n = min(n_total, 2_000_000)
+    n = min(n_total, int(os.environ.get("STAMPS_ROWS", 2_000_000)))
     data = generate_pairs(n, nf, nc, seed=42, device=dev)
     meta = {k: data[k] for k in ("n_firm_numeric", "firm_cat_counts", "n_ceo_numeric", "ceo_cat_counts")}
     cfg = Config()

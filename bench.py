@@ -281,13 +281,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("CEO_BENCH_SHARE_GPU"):  # rehearsal: every rank on GPU 0 (one-GPU box)
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1 or args.dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        # CEO_BENCH_BACKEND=gloo: rehearsal of the N > 1 flow on a one-GPU box
+        # (RCCL refuses two ranks on one device); gloo steps run eagerly.
+        backend = os.environ.get("CEO_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
         pg = dist.group.WORLD
 
     from ceo_firm_matching import CEOFirmMatcher, Config
@@ -313,7 +321,7 @@ def main():
     # hipGraph replay of whole steps at every world size: the RCCL all-reduce
     # of the data-parallel step is captured with the kernels (no host work
     # per step); --no-graph launches every step eagerly.
-    use_graph = not args.no_graph
+    use_graph = not args.no_graph and (pg is None or dist.get_backend(pg) == "nccl")
     step_fn = lambda: tr.step_cycle(rows, B, n_batches)  # noqa: E731
     for _ in range(args.warmup):
         step_fn()
@@ -322,20 +330,34 @@ def main():
     graph, chunk = None, 1
     if use_graph:
         chunk = max(c for c in range(1, 17) if args.steps % c == 0)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                step_fn()
-        torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for _ in range(chunk):
-                step_fn()
-        graph.replay()  # one more warm replay
+        ok = 1
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    step_fn()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):  # recorded only: nothing executes during capture
+                for _ in range(chunk):
+                    step_fn()
+        except Exception as e:  # capture unsupported here: every rank falls back to eager steps
+            print(f"bench: graph capture failed ({e!r}); eager steps", file=sys.stderr)
+            ok, graph = 0, None
+        if pg is not None:  # all ranks replay, or none does
+            flag = torch.tensor([ok], device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                graph = None
+        if graph is not None:
+            graph.replay()  # one more warm replay
         torch.cuda.synchronize()
         if pg is not None:
             dist.barrier()
+        if graph is None:
+            chunk = 1
 
     tr.pop_loss_sum(read=False)
     if pg is not None:

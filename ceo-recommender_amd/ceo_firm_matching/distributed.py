@@ -36,6 +36,9 @@ def average_gradients_(flat_grad: torch.Tensor, group=None) -> torch.Tensor:
     if not (dist.is_available() and dist.is_initialized()):
         return flat_grad
     w = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":  # RCCL averages inside the collective (no extra kernel)
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=group)
+        return flat_grad
     dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
     if w > 1:
         flat_grad.mul_(1.0 / w)

@@ -1,10 +1,6 @@
-mkdir -p gpurun_out/s3; export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -x > gpurun_out/s3/pt.log 2>&1 || { tail gpurun_out/s3/pt.log; exit 1; }
-tail -1 gpurun_out/s3/pt.log
-STAMPS_ROWS=10000000 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s3/p -o run --output-format csv -- python3 tools/stamps_prod.py > gpurun_out/s3/p.log 2>&1 || { tail gpurun_out/s3/p.log; exit 1; }
-python - <<PY
-import csv,glob
-f=glob.glob("gpurun_out/s3/p/**/*kernel_stats.csv",recursive=True)[0]
-for r in csv.DictReader(open(f)):
-    if "tt::" in r["Name"]: print(r["Name"][:50], r["Calls"], round(float(r["AverageNs"])/1000,2))
-PY
+mkdir -p gpurun_out/dp2; export TMPDIR=/tmp
+CEO_BENCH_SHARE_GPU=1 CEO_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/dp2/out.json 2> gpurun_out/dp2/err.log; rc=$?
+echo "rc=$rc"; tail -c 2500 gpurun_out/dp2/out.json; grep -iE "error|Traceback" -A3 gpurun_out/dp2/err.log | head -30
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --dp --no-graph --no-cpu-baseline --no-extras > gpurun_out/dp2/dp_eager.json 2>gpurun_out/dp2/dp_eager.err || exit 1
+python -c "import json;d=json.load(open('gpurun_out/dp2/dp_eager.json'));print('dp eager world1', d['value'], d['ms_per_step'])"

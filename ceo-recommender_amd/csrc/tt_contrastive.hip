@@ -32,22 +32,51 @@ constexpr int TM = WM / 16, TN = WN / 16;                    // 4 x 8 MFMA tiles
 constexpr int TILE = 256;                                    // floats per 16x16 tile
 constexpr float SUM_MIN = 1e-30f;  // row/col sums below this: exp underflow (reported)
 
-// LDS operand layouts (floats): "MK" = [m][k] (k contiguous, b128 reads),
-// "KM" = [k][m] (m contiguous, b32 reads).  +4 padding.
-constexpr int LD_MK = BK + 4;
-constexpr int LD_KM = BM + 4;  // BM == BN
-constexpr int OPND_FLOATS = (BM * LD_MK > BK * LD_KM) ? BM * LD_MK : BK * LD_KM;
-constexpr int STAGE_FLOATS = 2 * OPND_FLOATS;  // A + B
-constexpr size_t LDS_BYTES = sizeof(float) * 2 * STAGE_FLOATS;  // double buffered
+// Operand precision: fp32 through the bf16 MFMA.  Each fp32 value x is
+// split exactly into three bf16 planes x = h + m + l (8 significand bits
+// each, round-to-nearest), and a product is the six plane products whose
+// magnitude is >= 2^-16 of h*h:
+//     x*y ~= l*h + m*m + h*l + m*h + h*m + h*h
+// (the dropped m*l, l*m, l*l terms are <= ~2^-24 relative, i.e. fp32's own
+// rounding).  Every plane product is exact in the fp32 accumulator, so the
+// GEMM is fp32-accurate while running v_mfma_f32_16x16x32_bf16: 6 MFMAs of
+// 16 cycles per 32-deep K step instead of 8 fp32 MFMAs of 32 cycles (2.7x).
+// The split happens once per element while staging into LDS.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int NPL = 3;                // planes h, m, l
+constexpr int LDK = BK + 8;           // bf16 per LDS row (80 B: 16-B aligned rows)
+constexpr int PLANE = BM * LDK;       // bf16 per plane of one operand (BM == BN)
+constexpr int OPND = NPL * PLANE;     // bf16 per operand
+constexpr size_t LDS_BYTES = sizeof(uint16_t) * 2 * OPND;  // A + B, single buffer (120 KB)
 
-// Where an operand comes from and how it is laid out in LDS.
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+__device__ __forceinline__ float bf16_val(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+// split two values at once: packed planes (lo half = first value)
+__device__ __forceinline__ void split3x2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = pk_bf16(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = pk_bf16(r0, r1);
+  l = pk_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xffff0000u));
+}
+__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = bf16_bits(x);
+  const float r1 = x - bf16_val(h);  // exact
+  m = bf16_bits(r1);
+  l = bf16_bits(r1 - bf16_val(m));   // exact residual, rounded to bf16
+}
+
+// Where an operand comes from.  LDS always holds [m][k] bf16 planes.
 enum Src : int {
-  SRC_MK = 0,       // row-major G[m][k] (ld)            -> LDS [m][k]
-  SRC_KM = 1,       // row-major G[k][m] (ld)            -> LDS [k][m]
-  SRC_E_AS_KM = 2,  // E tiles, m = E row i, k = E col j -> LDS [k][m]  (dF = E' C)
-  SRC_E_AS_MK = 3,  // E tiles, m = E col j, k = E row i -> LDS [m][k]  (dC = E'^T F)
+  SRC_MK = 0,       // row-major G[m][k] (ld): a thread's float4 runs along k
+  SRC_KM = 1,       // row-major G[k][m] (ld): a thread's float4 runs along m
+  SRC_E_AS_KM = 2,  // E tiles, m = E row i, k = E col j (float4 along m)   (dF = E' C)
+  SRC_E_AS_MK = 3,  // E tiles, m = E col j, k = E row i (float4 along k)   (dC = E'^T F)
 };
-__host__ __device__ constexpr bool lds_mk(int s) { return s == SRC_MK || s == SRC_E_AS_MK; }
 
 struct Opnd {
   const float* p;
@@ -129,8 +158,124 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
   }
 }
 
+// split the staged float4s into the three bf16 planes of LDS [m][k]
 template <int S>
-__device__ __forceinline__ void store_opnd(float* L, const float4 (&v)[4]) {
+__device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = (int)threadIdx.x + q * NTH;
+    int m, k;
+    bool along_k;
+    if constexpr (S == SRC_MK) {
+      m = e >> 3; k = (e & 7) * 4; along_k = true;
+    } else if constexpr (S == SRC_KM) {
+      k = e >> 6; m = (e & 63) * 4; along_k = false;
+    } else {
+      const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
+      if constexpr (S == SRC_E_AS_KM) {  // float4 = 4 consecutive E rows i = m
+        m = 16 * tm + 4 * (ln >> 4); k = 16 * tk + (ln & 15); along_k = false;
+      } else {  // float4 = 4 consecutive E rows i = k
+        m = 16 * tm + (ln & 15); k = 16 * tk + 4 * (ln >> 4); along_k = true;
+      }
+    }
+    uint32_t h01, m01, l01, h23, m23, l23;  // packed bf16 pairs of the three planes
+    split3x2(v[q].x, v[q].y, h01, m01, l01);
+    split3x2(v[q].z, v[q].w, h23, m23, l23);
+    if (along_k) {  // 4 consecutive k of row m: one 8-byte write per plane
+      uint16_t* d = L + m * LDK + k;
+      *reinterpret_cast<uint2*>(d) = make_uint2(h01, h23);
+      *reinterpret_cast<uint2*>(d + PLANE) = make_uint2(m01, m23);
+      *reinterpret_cast<uint2*>(d + 2 * PLANE) = make_uint2(l01, l23);
+    } else {  // 4 consecutive m at one k: transposing 2-byte writes
+      const uint32_t hh[2] = {h01, h23}, mm[2] = {m01, m23}, ll[2] = {l01, l23};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        uint16_t* d = L + (m + s) * LDK + k;
+        const int sh = (s & 1) * 16;
+        d[0] = (uint16_t)(hh[s >> 1] >> sh);
+        d[PLANE] = (uint16_t)(mm[s >> 1] >> sh);
+        d[2 * PLANE] = (uint16_t)(ll[s >> 1] >> sh);
+      }
+    }
+  }
+}
+
+// MFMA operand: 8 consecutive k (k = kk + 8g .. +7) of row m, one plane
+__device__ __forceinline__ bf16x8 frag(const uint16_t* L, int plane, int m, int g) {
+  return *reinterpret_cast<const bf16x8*>(L + plane * PLANE + m * LDK + 8 * g);
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// the six plane products, smallest first (fixed order: the diagonal kernel
+// replays exactly this sequence)
+constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+
+// Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T.  One LDS
+// stage (120 KB); the next chunk's global loads are in flight during the
+// MFMAs of the current one.
+template <int SA, int SB>
+__device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
+                                          uint16_t* smem, f32x4 (&acc)[TM][TN]) {
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
+  const int wm = w / NWN, wn = w % NWN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  float4 va[4], vb[4];
+  const int nch = (int)((ke - kb + BK - 1) / BK);
+  if (nch <= 0) return;
+  uint16_t* As = smem;
+  uint16_t* Bs = smem + OPND;
+  load_opnd<SA>(g_.A, m0, kb, va);
+  load_opnd<SB>(g_.B, n0, kb, vb);
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();  // the previous chunk's fragments have been read
+    store_opnd<SA>(As, va);
+    store_opnd<SB>(Bs, vb);
+    __syncthreads();
+    if (c + 1 < nch) {
+      load_opnd<SA>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
+      load_opnd<SB>(g_.B, n0, kb + (int64_t)(c + 1) * BK, vb);
+    }
+    bf16x8 a[TM][NPL];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) a[i][p] = frag(As, p, wm * WM + 16 * i + r, g);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bf16x8 b[NPL];
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) b[p] = frag(Bs, p, wn * WN + 16 * j + r, g);
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = mfma_bf16(a[i][PA[q]], b[PB[q]], acc[i][j]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Exact-fp32 MFMA core (v_mfma_f32_16x16x4_f32), double-buffered fp32 LDS.
+// Used by the gradient GEMMs, whose E operand would need a transposing
+// plane split (see the bf16x3 core above for the similarity GEMMs).
+// ---------------------------------------------------------------------------
+// LDS operand layouts (floats): "MK" = [m][k] (k contiguous, b128 reads),
+// "KM" = [k][m] (m contiguous, b32 reads).  +4 padding.
+constexpr int LD_MK = BK + 4;
+constexpr int LD_KM = BM + 4;  // BM == BN
+constexpr int OPND_FLOATS = (BM * LD_MK > BK * LD_KM) ? BM * LD_MK : BK * LD_KM;
+constexpr int STAGE_FLOATS = 2 * OPND_FLOATS;  // A + B
+constexpr size_t LDS_BYTES_F32 = sizeof(float) * 2 * STAGE_FLOATS;  // double buffered (144 KB)
+__host__ __device__ constexpr bool lds_mk(int s) { return s == SRC_MK || s == SRC_E_AS_MK; }
+
+template <int S>
+__device__ __forceinline__ void store_opnd_f32(float* L, const float4 (&v)[4]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int e = (int)threadIdx.x + q * NTH;
@@ -153,7 +298,7 @@ __device__ __forceinline__ void store_opnd(float* L, const float4 (&v)[4]) {
 
 // MFMA fragment of a 16-wide K slice: 4 consecutive k (k = kk + 4g + s)
 template <bool MK>
-__device__ __forceinline__ float4 frag(const float* L, int m, int kk, int g) {
+__device__ __forceinline__ float4 frag_f32(const float* L, int m, int kk, int g) {
   if constexpr (MK) {
     return *reinterpret_cast<const float4*>(L + m * LD_MK + kk + 4 * g);
   } else {
@@ -164,7 +309,7 @@ __device__ __forceinline__ float4 frag(const float* L, int m, int kk, int g) {
 
 // Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T
 template <int SA, int SB>
-__device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
+__device__ __forceinline__ void gemm_loop_f32(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
                                           float* smem, f32x4 (&acc)[TM][TN]) {
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   const int wm = w / NWN, wn = w % NWN;
@@ -177,8 +322,8 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
   if (nch <= 0) return;
   load_opnd<SA>(g_.A, m0, kb, va);
   load_opnd<SB>(g_.B, n0, kb, vb);
-  store_opnd<SA>(smem, va);
-  store_opnd<SB>(smem + OPND_FLOATS, vb);
+  store_opnd_f32<SA>(smem, va);
+  store_opnd_f32<SB>(smem + OPND_FLOATS, vb);
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
     float* cur = smem + (c & 1) * STAGE_FLOATS;
@@ -192,18 +337,18 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
     for (int kk = 0; kk < BK; kk += 16) {
       float4 a[TM];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = frag<lds_mk(SA)>(As, wm * WM + 16 * i + r, kk, g);
+      for (int i = 0; i < TM; ++i) a[i] = frag_f32<lds_mk(SA)>(As, wm * WM + 16 * i + r, kk, g);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {  // one B fragment live at a time (register budget)
-        const float4 b = frag<lds_mk(SB)>(Bs, wn * WN + 16 * j + r, kk, g);
+        const float4 b = frag_f32<lds_mk(SB)>(Bs, wn * WN + 16 * j + r, kk, g);
 #pragma unroll
         for (int i = 0; i < TM; ++i) mfma_k16(a[i], b, acc[i][j]);
       }
     }
     if (c + 1 < nch) {
       float* nxt = smem + ((c + 1) & 1) * STAGE_FLOATS;
-      store_opnd<SA>(nxt, va);
-      store_opnd<SB>(nxt + OPND_FLOATS, vb);
+      store_opnd_f32<SA>(nxt, va);
+      store_opnd_f32<SB>(nxt + OPND_FLOATS, vb);
     }
     __syncthreads();
   }
@@ -224,7 +369,7 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t nblk) {
 // ---------------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(NTH) void k_nce_sim(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int64_t nblk = (int64_t)gridDim.x;
   const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
   const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
@@ -303,10 +448,21 @@ __global__ __launch_bounds__(NTH) void k_nce_sim(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// diagonal of F C^T with the GEMM's own arithmetic (same MFMA sequence per
-// 16x16 tile, same K order) -> bitwise the value the tiled GEMM produces.
-// One wave per 16-row tile; C rows row0 + i.
+// diagonal of F C^T with the GEMM's own arithmetic (same plane split, same
+// six-MFMA sequence per 32-deep K step, same K order) -> bitwise the value
+// the tiled GEMM produces.  One wave per 16-row tile; C rows row0 + i.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void split8(const float (&x)[8], bf16x8 (&pl)[NPL]) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    uint16_t h, m, l;
+    split3(x[s], h, m, l);
+    pl[0][s] = __builtin_bit_cast(__bf16, h);
+    pl[1][s] = __builtin_bit_cast(__bf16, m);
+    pl[2][s] = __builtin_bit_cast(__bf16, l);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_nce_diag(const float* __restrict__ F, const float* __restrict__ C,
                                                   int64_t m, int64_t n, int d, int64_t row0, float scale,
                                                   float* __restrict__ diag) {
@@ -315,13 +471,23 @@ __global__ __launch_bounds__(256) void k_nce_diag(const float* __restrict__ F, c
   const int64_t i = t * 16 + r;  // row of this lane (A operand) and column (B operand)
   const bool okf = i < m, okc = (row0 + i) < n && (row0 + i) >= 0;
   f32x4 acc = zero4();
-  for (int k0 = 0; k0 < d; k0 += 16) {
-    const int k = k0 + 4 * g;
-    const bool kk = k < d;
-    float4 av = make_float4(0.f, 0.f, 0.f, 0.f), bv = av;
-    if (okf && kk) av = *reinterpret_cast<const float4*>(F + i * d + k);
-    if (okc && kk) bv = *reinterpret_cast<const float4*>(C + (row0 + i) * d + k);
-    mfma_k16(av, bv, acc);
+  for (int k0 = 0; k0 < d; k0 += BK) {
+    float xa[8], xb[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = k0 + 8 * g + 4 * h;
+      const bool kk = k < d;
+      float4 av = make_float4(0.f, 0.f, 0.f, 0.f), bv = av;
+      if (okf && kk) av = *reinterpret_cast<const float4*>(F + i * d + k);
+      if (okc && kk) bv = *reinterpret_cast<const float4*>(C + (row0 + i) * d + k);
+      xa[4 * h + 0] = av.x; xa[4 * h + 1] = av.y; xa[4 * h + 2] = av.z; xa[4 * h + 3] = av.w;
+      xb[4 * h + 0] = bv.x; xb[4 * h + 1] = bv.y; xb[4 * h + 2] = bv.z; xb[4 * h + 3] = bv.w;
+    }
+    bf16x8 a[NPL], b[NPL];
+    split8(xa, a);
+    split8(xb, b);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) acc = mfma_bf16(a[PA[q]], b[PB[q]], acc);
   }
   // acc[q] = C[row 4g+q][col r]; the diagonal is row == col
 #pragma unroll
@@ -335,7 +501,7 @@ __global__ __launch_bounds__(256) void k_nce_diag(const float* __restrict__ F, c
 // ---------------------------------------------------------------------------
 template <int SA>
 __global__ __launch_bounds__(NTH) void k_nce_dgrad(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int64_t nblk = (int64_t)gridDim.x;
   const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
   const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
@@ -344,7 +510,7 @@ __global__ __launch_bounds__(NTH) void k_nce_dgrad(GemmArgs a) {
   const int64_t kb = split * a.k_per_split;
   const int64_t ke = min(kb + a.k_per_split, a.A.kdim);
   f32x4 acc[TM][TN];
-  gemm_loop<SA, SRC_KM>(a, m0, n0, kb, ke, smem, acc);
+  gemm_loop_f32<SA, SRC_KM>(a, m0, n0, kb, ke, reinterpret_cast<float*>(smem), acc);
   const int w = wave_id(), l = lane_id();
   const int wm = w / NWN, wn = w % NWN;
 #pragma unroll

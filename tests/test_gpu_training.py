@@ -134,3 +134,18 @@ def test_data_parallel_step_two_ranks_one_gpu():
     for rank, err, where in res:
         assert err < 1e-5, (rank, err, where)
     assert all(p.exitcode == 0 for p in ps)
+
+
+def test_interaction_grid_on_fused_eval_forward():
+    """The batched heatmap grid (one tt_forward) equals the CPU evaluation of
+    the same weights."""
+    _need_gpu()
+    from test_consumers import _setup
+    from ceo_firm_matching.visualization import interaction_grid
+    cfg, proc, model, _ = _setup()
+    ref = [interaction_grid(model, proc, xf, yf)[2] for xf, yf in (("logatw", "Age"), ("maxedu", "rdintw"))]
+    proc.cfg.DEVICE = torch.device("cuda")
+    model = model.to("cuda")
+    got = [interaction_grid(model, proc, xf, yf)[2] for xf, yf in (("logatw", "Age"), ("maxedu", "rdintw"))]
+    for g_, r_ in zip(got, ref):
+        assert normwise(g_, r_) < 1e-5

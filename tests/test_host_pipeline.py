@@ -107,7 +107,7 @@ def test_cli_synthetic_runs(tmp_path):
     env = dict(os.environ, PYTHONPATH=PKG_PARENT, CEO_TT_OUTPUT=str(tmp_path), HIP_VISIBLE_DEVICES="")
     out = tmp_path / "sd.pt"
     r = subprocess.run([sys.executable, "-m", "ceo_firm_matching.cli", "--synthetic", "--epochs", "1",
-                        "--save", str(out)], cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                        "--no-plots", "--save", str(out)], cwd=str(tmp_path), env=env, capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Using SYNTHETIC data..." in r.stdout

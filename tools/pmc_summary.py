@@ -7,7 +7,7 @@ import sys
 
 root = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{root}/**/run_counter_collection.csv", recursive=True)):
     for row in csv.DictReader(open(f)):
         k = row["Kernel_Name"]
         agg[k][row["Counter_Name"]].append(float(row["Counter_Value"]))

@@ -690,9 +690,9 @@ static std::once_flag g_nce_attr;
 static void nce_attrs() {
   std::call_once(g_nce_attr, [] {
     const void* ks[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>,
-                        (const void*)k_nce_dgrad<SRC_E_AS_KM>, (const void*)k_nce_dgrad<SRC_E_AS_MK>};
+                        (const void*)k_nce_dgrad<SRC_E_ROWS>, (const void*)k_nce_dgrad<SRC_E_AS_MK>};
     for (const void* k : ks)
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max(LDS_BYTES, LDS_BYTES_F32));
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
   });
 }
 
@@ -807,7 +807,7 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.p_nti = L.nti;
     g.p_ntj = L.pntj;
     const dim3 grid((unsigned)(((m + BM - 1) / BM) * g.n_blocks_n), (unsigned)L.split_f);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_KM>, grid, dim3(NTH), LDS_BYTES_F32, s, g);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_ROWS>, grid, dim3(NTH), LDS_BYTES, s, g);
     const int64_t el = L.nti * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_f, L.nti, L.pntj, m, d, scale, corr, c, n, row0, df);
@@ -826,7 +826,7 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.p_nti = L.ntj;
     g.p_ntj = L.pntj;
     const dim3 grid((unsigned)(((n + BM - 1) / BM) * g.n_blocks_n), (unsigned)L.split_c);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(NTH), LDS_BYTES_F32, s, g);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(NTH), LDS_BYTES, s, g);
     const int64_t el = L.ntj * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_c, L.ntj, L.pntj, n, d, scale, corr, f, m, -row0, dc);

@@ -72,15 +72,31 @@ __device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16
 
 // Where an operand comes from.  LDS always holds [m][k] bf16 planes.
 enum Src : int {
-  SRC_MK = 0,       // row-major G[m][k] (ld): a thread's float4 runs along k
-  SRC_KM = 1,       // row-major G[k][m] (ld): a thread's float4 runs along m
-  SRC_E_AS_KM = 2,  // E tiles, m = E row i, k = E col j (float4 along m)   (dF = E' C)
-  SRC_E_AS_MK = 3,  // E tiles, m = E col j, k = E row i (float4 along k)   (dC = E'^T F)
+  // every source hands a thread 4 consecutive k, so the split planes are
+  // written along k (8-byte LDS writes, no transposition)
+  SRC_MK = 0,       // row-major G[m][k] (ld): one float4 along k
+  SRC_E_AS_MK = 3,  // E tiles, m = E col j, k = E row i: the tile's float4 (4 rows i)  (dC = E'^T F)
+  SRC_KROWS = 4,    // row-major G[k][m] (ld): 4 scalar loads down k, lanes along m (coalesced)
+  SRC_E_ROWS = 5,   // E tiles, m = E row i, k = E col j: 4 scalar loads along j     (dF = E' C)
 };
+
+// Buffer resources (SGPR base + 32-bit lane offsets; reads outside
+// [0, bytes) return 0, which zero-fills every partial tile for free).
+constexpr uint32_t BUF_OOB = 0xFFFFFFFFu;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes) {
+  const int64_t nb = bytes < 0 ? 0 : (bytes > 0x7FFFFFFF ? 0x7FFFFFFF : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)nb, 0x00020000);
+}
+__device__ __forceinline__ float buf_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));  // the builtin returns the bits
+}
+__device__ __forceinline__ float4 buf_f32x4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
 struct Opnd {
   const float* p;
-  int64_t ld;      // row stride (SRC_MK / SRC_KM)
+  int64_t ld;      // row stride (SRC_MK / SRC_KROWS)
   int64_t mdim;    // extent along m (rows of the output side)
   int64_t kdim;    // extent along k
   int64_t nti, ntj;  // E tile grid (SRC_E_*)
@@ -113,47 +129,65 @@ struct GemmArgs {
 // ---- global -> registers (4 float4 per thread per operand per K chunk) ----
 template <int S>
 __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0, float4 (&v)[4]) {
+  if constexpr (S == SRC_MK) {  // tile BM x BK from G[m][k]: 8 float4 per row
+    const auto rs = buf_rsrc(o.p + m0 * o.ld, (o.mdim - m0) * o.ld * 4);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = (int)threadIdx.x + q * NTH;
-    if constexpr (S == SRC_MK) {  // tile BM x BK: 8 float4 per row
+    for (int q = 0; q < 4; ++q) {
+      const int e = (int)threadIdx.x + q * NTH;
       const int r = e >> 3, kq = (e & 7) * 4;
-      const int64_t gm = m0 + r, gk = k0 + kq;
-      const bool ok = gm < o.mdim && gk < o.kdim;
-      const float* p = o.p + (ok ? gm * o.ld + gk : 0);
-      const float4 x = *reinterpret_cast<const float4*>(p);
-      v[q] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else if constexpr (S == SRC_KM) {  // tile BK x BM: 64 float4 per k row
-      const int kr = e >> 6, mq = (e & 63) * 4;
-      const int64_t gk = k0 + kr, gm = m0 + mq;
-      const bool ok = gk < o.kdim && gm < o.mdim;
-      const float* p = o.p + (ok ? gk * o.ld + gm : 0);
-      const float4 x = *reinterpret_cast<const float4*>(p);
-      v[q] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {  // E tiles: 32 tiles of 1 KB (16 along m x 2 along k), lane -> float4
+      const bool ok = k0 + kq < o.kdim;
+      v[q] = buf_f32x4(rs, ok ? (uint32_t)((r * o.ld + k0 + kq) * 4) : BUF_OOB);
+    }
+  } else if constexpr (S == SRC_KROWS) {  // G[k][m]: 256 m (lanes) x 8 k-quads, 4 scalar loads
+    const auto rs = buf_rsrc(o.p + k0 * o.ld, (o.kdim - k0) * o.ld * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = (int)threadIdx.x + q * NTH;
+      const int ml = e & 255, kq = (e >> 8) * 4;
+      const bool ok = m0 + ml < o.mdim;
+      float x[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        x[c] = buf_f32(rs, ok ? (uint32_t)(((kq + c) * o.ld + m0 + ml) * 4) : BUF_OOB);
+      v[q] = make_float4(x[0], x[1], x[2], x[3]);
+    }
+  } else if constexpr (S == SRC_E_ROWS) {  // E'(i, j..j+3): 256 i x 8 j-quads
+    const int64_t ti0 = m0 >> 4, tj0 = k0 >> 4;
+    const int64_t tiles = (o.nti - ti0) * o.ntj - tj0;  // tiles from (ti0, tj0) to the end of E
+    const auto rs = buf_rsrc(o.p + (ti0 * o.ntj + tj0) * TILE, tiles * TILE * 4);
+    const auto ra = buf_rsrc(o.a, o.nti * 16 * 4), rb = buf_rsrc(o.b, o.ntj * 16 * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = (int)threadIdx.x + q * NTH;
+      const int il = e >> 3, jq = (e & 7) * 4;
+      const int64_t gi = m0 + il, gj = k0 + jq;
+      const bool ok = (gj >> 4) < o.ntj && (gi >> 4) < o.nti;
+      // element (ii, jj) of a tile: lane jj + 16 (ii / 4), slot ii % 4
+      const uint32_t base = (uint32_t)(((il >> 4) * o.ntj + (jq >> 4)) * TILE +
+                                       ((gj & 15) + 16 * ((gi & 15) >> 2)) * 4 + (gi & 3));
+      const float ai = buf_f32(ra, ok ? (uint32_t)(gi * 4) : BUF_OOB);
+      const float4 bj = buf_f32x4(rb, ok ? (uint32_t)(gj * 4) : BUF_OOB);
+      float x[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[c] = buf_f32(rs, ok ? (base + 4 * c) * 4 : BUF_OOB);
+      v[q] = make_float4(x[0] * (ai + bj.x), x[1] * (ai + bj.y), x[2] * (ai + bj.z), x[3] * (ai + bj.w));
+    }
+  } else if constexpr (S == SRC_E_AS_MK) {  // E tiles as [m = j][k = i]: 16 j-tiles x 2 i-tiles
+    const int64_t tj0 = m0 >> 4, ti0 = k0 >> 4;
+    const int64_t tiles = (o.nti - ti0) * o.ntj - tj0;
+    const auto rs = buf_rsrc(o.p + (ti0 * o.ntj + tj0) * TILE, tiles * TILE * 4);
+    const auto ra = buf_rsrc(o.a, o.nti * 16 * 4), rb = buf_rsrc(o.b, o.ntj * 16 * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = (int)threadIdx.x + q * NTH;
       const int t = e >> 6, ln = e & 63;
       const int tm = t >> 1, tk = t & 1;
-      int64_t ti, tj;  // E tile coordinates (i = E row block, j = E col block)
-      if constexpr (S == SRC_E_AS_KM) {
-        ti = m0 / 16 + tm;
-        tj = k0 / 16 + tk;
-      } else {
-        tj = m0 / 16 + tm;
-        ti = k0 / 16 + tk;
-      }
+      const int64_t tj = tj0 + tm, ti = ti0 + tk;
       const bool ok = ti < o.nti && tj < o.ntj;
-      const f32x4 x = __builtin_nontemporal_load(
-          reinterpret_cast<const f32x4*>(o.p + (ok ? (ti * o.ntj + tj) * TILE : 0) + ln * 4));
-      // E' = E (a_i + b_j): rows i = 16 ti + 4 (ln>>4) + s, column j = 16 tj + (ln & 15)
-      const int64_t i0 = (ok ? ti : 0) * 16 + 4 * (ln >> 4);
-      const float4 ai = *reinterpret_cast<const float4*>(o.a + i0);
-      const float bj = o.b[(ok ? tj : 0) * 16 + (ln & 15)];
-      float4 y;
-      y.x = x[0] * (ai.x + bj);
-      y.y = x[1] * (ai.y + bj);
-      y.z = x[2] * (ai.z + bj);
-      y.w = x[3] * (ai.w + bj);
-      v[q] = ok ? y : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x = buf_f32x4(rs, ok ? (uint32_t)(((tk * o.ntj + tm) * TILE + ln * 4) * 4) : BUF_OOB);
+      const float4 ai = buf_f32x4(ra, ok ? (uint32_t)((ti * 16 + 4 * (ln >> 4)) * 4) : BUF_OOB);
+      const float bj = buf_f32(rb, ok ? (uint32_t)((tj * 16 + (ln & 15)) * 4) : BUF_OOB);
+      v[q] = make_float4(x.x * (ai.x + bj), x.y * (ai.y + bj), x.z * (ai.z + bj), x.w * (ai.w + bj));
     }
   }
 }
@@ -164,39 +198,22 @@ __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[4]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int e = (int)threadIdx.x + q * NTH;
-    int m, k;
-    bool along_k;
-    if constexpr (S == SRC_MK) {
-      m = e >> 3; k = (e & 7) * 4; along_k = true;
-    } else if constexpr (S == SRC_KM) {
-      k = e >> 6; m = (e & 63) * 4; along_k = false;
-    } else {
+    int m, k;  // the thread's float4 holds k .. k+3 of row m
+    if constexpr (S == SRC_MK || S == SRC_E_ROWS) {
+      m = e >> 3; k = (e & 7) * 4;
+    } else if constexpr (S == SRC_KROWS) {
+      m = e & 255; k = (e >> 8) * 4;
+    } else {  // SRC_E_AS_MK: the tile float4 = 4 consecutive E rows i = k
       const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
-      if constexpr (S == SRC_E_AS_KM) {  // float4 = 4 consecutive E rows i = m
-        m = 16 * tm + 4 * (ln >> 4); k = 16 * tk + (ln & 15); along_k = false;
-      } else {  // float4 = 4 consecutive E rows i = k
-        m = 16 * tm + (ln & 15); k = 16 * tk + 4 * (ln >> 4); along_k = true;
-      }
+      m = 16 * tm + (ln & 15); k = 16 * tk + 4 * (ln >> 4);
     }
     uint32_t h01, m01, l01, h23, m23, l23;  // packed bf16 pairs of the three planes
     split3x2(v[q].x, v[q].y, h01, m01, l01);
     split3x2(v[q].z, v[q].w, h23, m23, l23);
-    if (along_k) {  // 4 consecutive k of row m: one 8-byte write per plane
-      uint16_t* d = L + m * LDK + k;
-      *reinterpret_cast<uint2*>(d) = make_uint2(h01, h23);
-      *reinterpret_cast<uint2*>(d + PLANE) = make_uint2(m01, m23);
-      *reinterpret_cast<uint2*>(d + 2 * PLANE) = make_uint2(l01, l23);
-    } else {  // 4 consecutive m at one k: transposing 2-byte writes
-      const uint32_t hh[2] = {h01, h23}, mm[2] = {m01, m23}, ll[2] = {l01, l23};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        uint16_t* d = L + (m + s) * LDK + k;
-        const int sh = (s & 1) * 16;
-        d[0] = (uint16_t)(hh[s >> 1] >> sh);
-        d[PLANE] = (uint16_t)(mm[s >> 1] >> sh);
-        d[2 * PLANE] = (uint16_t)(ll[s >> 1] >> sh);
-      }
-    }
+    uint16_t* d = L + m * LDK + k;  // one 8-byte write per plane
+    *reinterpret_cast<uint2*>(d) = make_uint2(h01, h23);
+    *reinterpret_cast<uint2*>(d + PLANE) = make_uint2(m01, m23);
+    *reinterpret_cast<uint2*>(d + 2 * PLANE) = make_uint2(l01, l23);
   }
 }
 
@@ -257,100 +274,6 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
 #pragma unroll
         for (int i = 0; i < TM; ++i) acc[i][j] = mfma_bf16(a[i][PA[q]], b[PB[q]], acc[i][j]);
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Exact-fp32 MFMA core (v_mfma_f32_16x16x4_f32), double-buffered fp32 LDS.
-// Used by the gradient GEMMs, whose E operand would need a transposing
-// plane split (see the bf16x3 core above for the similarity GEMMs).
-// ---------------------------------------------------------------------------
-// LDS operand layouts (floats): "MK" = [m][k] (k contiguous, b128 reads),
-// "KM" = [k][m] (m contiguous, b32 reads).  +4 padding.
-constexpr int LD_MK = BK + 4;
-constexpr int LD_KM = BM + 4;  // BM == BN
-constexpr int OPND_FLOATS = (BM * LD_MK > BK * LD_KM) ? BM * LD_MK : BK * LD_KM;
-constexpr int STAGE_FLOATS = 2 * OPND_FLOATS;  // A + B
-constexpr size_t LDS_BYTES_F32 = sizeof(float) * 2 * STAGE_FLOATS;  // double buffered (144 KB)
-__host__ __device__ constexpr bool lds_mk(int s) { return s == SRC_MK || s == SRC_E_AS_MK; }
-
-template <int S>
-__device__ __forceinline__ void store_opnd_f32(float* L, const float4 (&v)[4]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = (int)threadIdx.x + q * NTH;
-    float* d;
-    if constexpr (S == SRC_MK) {
-      d = L + (e >> 3) * LD_MK + (e & 7) * 4;
-    } else if constexpr (S == SRC_KM) {
-      d = L + (e >> 6) * LD_KM + (e & 63) * 4;
-    } else {
-      const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
-      // the lane's float4 runs along E rows i (4 consecutive)
-      if constexpr (S == SRC_E_AS_KM)  // m = i (consecutive), k = j
-        d = L + (16 * tk + (ln & 15)) * LD_KM + 16 * tm + 4 * (ln >> 4);
-      else  // m = j, k = i (consecutive)
-        d = L + (16 * tm + (ln & 15)) * LD_MK + 16 * tk + 4 * (ln >> 4);
-    }
-    *reinterpret_cast<float4*>(d) = v[q];
-  }
-}
-
-// MFMA fragment of a 16-wide K slice: 4 consecutive k (k = kk + 4g + s)
-template <bool MK>
-__device__ __forceinline__ float4 frag_f32(const float* L, int m, int kk, int g) {
-  if constexpr (MK) {
-    return *reinterpret_cast<const float4*>(L + m * LD_MK + kk + 4 * g);
-  } else {
-    const float* p = L + (kk + 4 * g) * LD_KM + m;
-    return make_float4(p[0], p[LD_KM], p[2 * LD_KM], p[3 * LD_KM]);
-  }
-}
-
-// Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T
-template <int SA, int SB>
-__device__ __forceinline__ void gemm_loop_f32(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
-                                          float* smem, f32x4 (&acc)[TM][TN]) {
-  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  const int wm = w / NWN, wn = w % NWN;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
-  float4 va[4], vb[4];
-  const int nch = (int)((ke - kb + BK - 1) / BK);
-  if (nch <= 0) return;
-  load_opnd<SA>(g_.A, m0, kb, va);
-  load_opnd<SB>(g_.B, n0, kb, vb);
-  store_opnd_f32<SA>(smem, va);
-  store_opnd_f32<SB>(smem + OPND_FLOATS, vb);
-  __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    float* cur = smem + (c & 1) * STAGE_FLOATS;
-    if (c + 1 < nch) {
-      load_opnd<SA>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
-      load_opnd<SB>(g_.B, n0, kb + (int64_t)(c + 1) * BK, vb);
-    }
-    const float* As = cur;
-    const float* Bs = cur + OPND_FLOATS;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 16) {
-      float4 a[TM];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = frag_f32<lds_mk(SA)>(As, wm * WM + 16 * i + r, kk, g);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {  // one B fragment live at a time (register budget)
-        const float4 b = frag_f32<lds_mk(SB)>(Bs, wn * WN + 16 * j + r, kk, g);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) mfma_k16(a[i], b, acc[i][j]);
-      }
-    }
-    if (c + 1 < nch) {
-      float* nxt = smem + ((c + 1) & 1) * STAGE_FLOATS;
-      store_opnd_f32<SA>(nxt, va);
-      store_opnd_f32<SB>(nxt + OPND_FLOATS, vb);
-    }
-    __syncthreads();
   }
 }
 
@@ -510,7 +433,7 @@ __global__ __launch_bounds__(NTH) void k_nce_dgrad(GemmArgs a) {
   const int64_t kb = split * a.k_per_split;
   const int64_t ke = min(kb + a.k_per_split, a.A.kdim);
   f32x4 acc[TM][TN];
-  gemm_loop_f32<SA, SRC_KM>(a, m0, n0, kb, ke, reinterpret_cast<float*>(smem), acc);
+  gemm_loop<SA, SRC_KROWS>(a, m0, n0, kb, ke, smem, acc);
   const int w = wave_id(), l = lane_id();
   const int wm = w / NWN, wn = w % NWN;
 #pragma unroll

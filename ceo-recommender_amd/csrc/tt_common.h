@@ -106,6 +106,87 @@ __device__ __forceinline__ void cl_gemm_tn(const f32x4& P, const f32x4& Q, f32x4
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
+// ---------------------------------------------------------------------------
+// fp32 through the bf16 MFMA (bf16x3 split).  Each fp32 value x is split
+// exactly into three bf16 planes x = h + m + l (round-to-nearest-even), and a
+// product is the six plane products whose magnitude is >= 2^-16 of h*h:
+//     x*y ~= l*h + m*m + h*l + m*h + h*m + h*h
+// (the dropped m*l, l*m, l*l terms are <= ~2^-24 relative: fp32's own
+// rounding).  Every plane product is exact in the fp32 accumulator, so a
+// 32-deep K step costs 6 v_mfma_f32_16x16x32_bf16 (16 cycles each) instead of
+// 8 v_mfma_f32_16x16x4_f32 (32 cycles each): 2.7x the fp32 MFMA rate.
+//   16x16x32 operand map: lane l holds A[m = l&15][k = 8(l>>4) + e] and
+//   B[k = 8(l>>4) + e][n = l&15] in element e; C as the fp32 form.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+__device__ __forceinline__ float bf16_val(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+// split two values at once: packed planes (lo half = first value)
+__device__ __forceinline__ void split3x2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = pk_bf16(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = pk_bf16(r0, r1);
+  l = pk_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xffff0000u));
+}
+__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = bf16_bits(x);
+  const float r1 = x - bf16_val(h);  // exact
+  m = bf16_bits(r1);
+  l = bf16_bits(r1 - bf16_val(m));   // exact residual, rounded to bf16
+}
+// 8 values -> three bf16x8 planes (element e = x[e])
+__device__ __forceinline__ void split8x3(const float (&x)[8], bf16x8 (&pl)[3]) {
+  u32x4 h, m, l;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t hh, mm, ll;
+    split3x2(x[2 * q], x[2 * q + 1], hh, mm, ll);
+    h[q] = hh;
+    m[q] = mm;
+    l[q] = ll;
+  }
+  pl[0] = __builtin_bit_cast(bf16x8, h);
+  pl[1] = __builtin_bit_cast(bf16x8, m);
+  pl[2] = __builtin_bit_cast(bf16x8, l);
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// the six plane products, smallest first (a fixed order: k_nce_diag replays
+// exactly this sequence)
+constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+__device__ __forceinline__ void mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4& c) {
+#pragma unroll
+  for (int q = 0; q < 6; ++q) c = mfma_bf16(a[PA[q]], b[PB[q]], c);
+}
+
+// gfx950 ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the
+// address of row q, 4 consecutive 16-bit columns (8-B aligned); lane i of the
+// group receives column i (chunk i>>2, element i&3) of the 4 rows, row q in
+// element q.  EXEC must be all ones.
+__device__ __forceinline__ s16x4 lds_tr16(const uint16_t* p) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+// two transposed reads -> one 16x16x32 operand (elements 0-3, 4-7)
+__device__ __forceinline__ bf16x8 tr_frag(const uint16_t* p0, const uint16_t* p1) {
+  const s16x4 x = lds_tr16(p0), y = lds_tr16(p1);
+  const u32x2 xu = __builtin_bit_cast(u32x2, x), yu = __builtin_bit_cast(u32x2, y);
+  return __builtin_bit_cast(bf16x8, (u32x4){xu[0], xu[1], yu[0], yu[1]});
+}
+
 // Cross-lane sums without LDS round trips (ds_bpermute costs a full LDS
 // latency per step and the compiler serialises dependent ones):
 //  * within a 16-lane row: DPP quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
@@ -158,9 +239,28 @@ __host__ __device__ __forceinline__ uint64_t dropout_key(uint64_t seed, uint64_t
   return mix64(seed * 0x9E3779B97F4A7C15ull + step * 0xD1B54A32D192ED03ull +
                (uint64_t)(tower * 2 + layer + 1) * 0x8CB92BA72F3D8DD7ull);
 }
-__device__ __forceinline__ bool dropout_keep(uint64_t key, uint64_t ctr, uint32_t thr) {
-  const uint64_t h = mix64(key + ctr * 0x9E3779B97F4A7C15ull);
-  return (uint32_t)(h >> 40) >= thr;
+// Per element (row, column) of one stream: a 32-bit avalanche permutation
+// (lowbias32) keyed per row, h = P(rk ^ column * 0x9E3779B9) with
+// rk = P(row ^ key_lo) + key_hi; keep iff the top 24 bits of h >= p * 2^24.
+// A bijection of the column within a row; the row key is shared by a row's
+// elements (one permutation per element, not one 64-bit mix), which matters:
+// the masks are recomputed wherever the forward or backward needs them.
+__host__ __device__ __forceinline__ uint32_t perm32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t dropout_row_key(uint64_t key, int64_t row) {
+  return perm32((uint32_t)row ^ (uint32_t)key) + (uint32_t)(key >> 32);
+}
+__device__ __forceinline__ bool dropout_keep_rk(uint32_t rk, int col, uint32_t thr) {
+  return (perm32(rk ^ ((uint32_t)col * 0x9E3779B9u)) >> 8) >= thr;
+}
+__device__ __forceinline__ bool dropout_keep(uint64_t key, int64_t row, int col, uint32_t thr) {
+  return dropout_keep_rk(dropout_row_key(key, row), col, thr);
 }
 
 // ---------------------------------------------------------------------------

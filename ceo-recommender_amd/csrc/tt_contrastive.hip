@@ -42,33 +42,12 @@ constexpr float SUM_MIN = 1e-30f;  // row/col sums below this: exp underflow (re
 // GEMM is fp32-accurate while running v_mfma_f32_16x16x32_bf16: 6 MFMAs of
 // 16 cycles per 32-deep K step instead of 8 fp32 MFMAs of 32 cycles (2.7x).
 // The split happens once per element while staging into LDS.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int NPL = 3;                // planes h, m, l
 constexpr int LDK = BK + 8;           // bf16 per LDS row (80 B: 16-B aligned rows)
 constexpr int PLANE = BM * LDK;       // bf16 per plane of one operand (BM == BN)
 constexpr int OPND = NPL * PLANE;     // bf16 per operand
 constexpr size_t LDS_BYTES = sizeof(uint16_t) * 2 * OPND;  // A + B, single buffer (120 KB)
 
-__device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
-__device__ __forceinline__ float bf16_val(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
-}
-// split two values at once: packed planes (lo half = first value)
-__device__ __forceinline__ void split3x2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
-  h = pk_bf16(x0, x1);
-  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
-  m = pk_bf16(r0, r1);
-  l = pk_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xffff0000u));
-}
-__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
-  h = bf16_bits(x);
-  const float r1 = x - bf16_val(h);  // exact
-  m = bf16_bits(r1);
-  l = bf16_bits(r1 - bf16_val(m));   // exact residual, rounded to bf16
-}
 
 // Where an operand comes from.  LDS always holds [m][k] bf16 planes.
 enum Src : int {
@@ -222,14 +201,6 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* L, int plane, int m, int 
   return *reinterpret_cast<const bf16x8*>(L + plane * PLANE + m * LDK + 8 * g);
 }
 
-__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// the six plane products, smallest first (fixed order: the diagonal kernel
-// replays exactly this sequence)
-constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
-constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
 
 // Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T.  One LDS
 // stage (120 KB); the next chunk's global loads are in flight during the

@@ -71,10 +71,10 @@ __device__ __forceinline__ void bn_coefs(const StepArgs& a, int H, const float* 
 
 // BN apply + ReLU + (train) dropout of one element.
 __device__ __forceinline__ float bn_relu_drop(float z, float mean, float alpha, float beta, bool drop,
-                                              uint64_t key, uint64_t ctr, uint32_t thr, float scale) {
+                                              uint32_t rk, int col, uint32_t thr, float scale) {
   float y = (z - mean) * alpha + beta;
   y = y > 0.f ? y : 0.f;
-  if (drop) y = dropout_keep(key, ctr, thr) ? y * scale : 0.f;
+  if (drop) y = dropout_keep_rk(rk, col, thr) ? y * scale : 0.f;
   return y;
 }
 
@@ -107,6 +107,47 @@ __device__ __forceinline__ void rep_sum(const float* rep, int stride, float* scr
   }
   __syncthreads();
 }
+
+// rep_sum of two equally shaped replica sets at once (one load round trip),
+// split in two so the caller can work while the loads are in flight:
+//   RepSum2<NTH, N> rs; rs.issue(rep0, rep1, stride);  ...  rs.finish(scratch, dst);
+// dst[0..N) from rep0, dst[N..2N) from rep1 (LDS, visible to the block after
+// finish).  scratch: NTH floats of LDS.
+template <int NTH, int N>
+struct RepSum2 {
+  static constexpr int N2 = 2 * N;
+  static constexpr int G0 = NTH / N2;
+  static constexpr int G = G0 < NREP ? G0 : NREP;
+  static constexpr int PER = NREP / G;
+  static_assert(NTH % N2 == 0 && NREP % G == 0, "replica groups");
+  float v[PER];
+  __device__ __forceinline__ void issue(const float* rep0, const float* rep1, int stride) {
+    const int c2 = (int)threadIdx.x % N2, grp = (int)threadIdx.x / N2;
+    if (grp < G) {
+      const float* rep = c2 < N ? rep0 : rep1;
+      const int c = c2 < N ? c2 : c2 - N;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) v[k] = rep[(grp + k * G) * stride + c];
+    }
+  }
+  __device__ __forceinline__ void finish(float* scratch, float* dst) {
+    const int c2 = (int)threadIdx.x % N2, grp = (int)threadIdx.x / N2;
+    if (grp < G) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) sum += v[k];
+      scratch[grp * N2 + c2] = sum;
+    }
+    __syncthreads();
+    if (threadIdx.x < N2) {
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < G; ++q) sum += scratch[q * N2 + threadIdx.x];
+      dst[threadIdx.x] = sum;
+    }
+    __syncthreads();
+  }
+};
 
 // Block-wide column sums of NT C-layout tiles into LDS `red` (ds_add_f32).
 template <int NT>
@@ -388,17 +429,18 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
   for (int k = 0; k < Z4PT; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int rl = e >> 4, c4 = (e & 15) * 4;
-    const uint64_t ctr = (uint64_t)(r0 + rl) * H0 + c4;
+    const uint32_t rk = dropout_row_key(key, r0 + rl);
     float4 o;
-    o.x = bn_relu_drop(z[k].x, cf[c4 + 0], cf[H0 + c4 + 0], cf[2 * H0 + c4 + 0], drop, key, ctr + 0, a.drop_thr, a.drop_scale);
-    o.y = bn_relu_drop(z[k].y, cf[c4 + 1], cf[H0 + c4 + 1], cf[2 * H0 + c4 + 1], drop, key, ctr + 1, a.drop_thr, a.drop_scale);
-    o.z = bn_relu_drop(z[k].z, cf[c4 + 2], cf[H0 + c4 + 2], cf[2 * H0 + c4 + 2], drop, key, ctr + 2, a.drop_thr, a.drop_scale);
-    o.w = bn_relu_drop(z[k].w, cf[c4 + 3], cf[H0 + c4 + 3], cf[2 * H0 + c4 + 3], drop, key, ctr + 3, a.drop_thr, a.drop_scale);
+    o.x = bn_relu_drop(z[k].x, cf[c4 + 0], cf[H0 + c4 + 0], cf[2 * H0 + c4 + 0], drop, rk, c4 + 0, a.drop_thr, a.drop_scale);
+    o.y = bn_relu_drop(z[k].y, cf[c4 + 1], cf[H0 + c4 + 1], cf[2 * H0 + c4 + 1], drop, rk, c4 + 1, a.drop_thr, a.drop_scale);
+    o.z = bn_relu_drop(z[k].z, cf[c4 + 2], cf[H0 + c4 + 2], cf[2 * H0 + c4 + 2], drop, rk, c4 + 2, a.drop_thr, a.drop_scale);
+    o.w = bn_relu_drop(z[k].w, cf[c4 + 3], cf[H0 + c4 + 3], cf[2 * H0 + c4 + 3], drop, rk, c4 + 3, a.drop_thr, a.drop_scale);
     *reinterpret_cast<float4*>(A0s + rl * LD + c4) = o;
   }
   if (a.train && threadIdx.x < H0) {
     const int c = threadIdx.x;
-    a0r[c] = bn_relu_drop(z0r, cf[c], cf[H0 + c], cf[2 * H0 + c], drop, key, (uint64_t)c, a.drop_thr, a.drop_scale);
+    a0r[c] = bn_relu_drop(z0r, cf[c], cf[H0 + c], cf[2 * H0 + c], drop, dropout_row_key(key, 0), c, a.drop_thr,
+                          a.drop_scale);
   }
   __syncthreads();
   TT_STAMP(1, 2);
@@ -445,34 +487,93 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_top : both towers' last layer, cosine score, loss, own-tower backward
+// k_top : both towers' last layer, cosine score, loss, own-tower backward.
+// Grid (tiles, 2): block (x, y) owns rows [x R, x R + R) and the backward of
+// tower y; both towers' forward is needed by both blocks of a tile.
+//
+// All four products run on the bf16x3 MFMA core (fp32-accurate, tt_common.h):
+//   forward   U^T[d][row]  = sum_h W8[d][h] A1[row][h]
+//             (A = W8 image rows, B = this lane's A1 slice straight from Z4)
+//   dA1^T[h][row]          = sum_d W8[d][h] dU[row][d]
+//             (A = W8 image via transposed reads, B = dU in the forward's
+//              accumulator layout -- no LDS round trip)
+//   dW8^T[h][d]            = sum_rows A1[row][h] dU[row][d]
+//   db8[d]                 = sum_rows dU[row][d]      (ones x dU, same loop)
+//             (A1 and dU images read transposed, rows = K)
+// The forward is computed transposed so that each row sits on one lane (its 4
+// lane groups split the latent dimension): the cosine's dot products are
+// in-lane sums plus one permlane reduction, and dU's registers of latent
+// tiles 2t, 2t+1 are exactly the 16x16x32 B operand of K step t of dA1^T.
+// dA1^T's hidden index is permuted (h = 8g + 4q + i for accumulator q,
+// register i, lane group g), so each lane ends with dY1 for its own row and
+// hidden columns 8g..8g+7 -- the columns it holds A1 and Z4 for: the ReLU /
+// dropout mask, the BN1-backward partials and the dY1 store (two float4)
+// need no data movement.
 // ---------------------------------------------------------------------------
 template <int NDT, int R>
 struct TopLds {
-  static constexpr int DP = 16 * NDT;
-  static constexpr int LDA = H1 + 4;
-  static constexpr int W8s = 0;
-  static constexpr int A1s = W8s + DP * LDA;
-  static constexpr int Z4s = A1s + R * LDA;
-  static constexpr int LDT = R + 4;            // transposed images [col][row]
-  static constexpr int A1T = Z4s + R * LDA;    // [32][R+4]
-  static constexpr int dUT = A1T + H1 * LDT;   // [DP][R+4]
-  static constexpr int db8 = dUT + DP * LDT;
-  static constexpr int cf1 = db8 + DP;
-  static constexpr int red = cf1 + 2 * 4 * H1;
-  static constexpr int scal = red + 2 * H1;  // [0] loss part [1] dls part
-  static constexpr int rsc = scal + 4;        // [4R] replica-sum scratch
-  static constexpr int rst = rsc + 4 * R;     // [2][2*32] BN1 moment sums S1|S2 per tower
-  static constexpr int total = rst + 4 * H1;
+  static constexpr int DP = 16 * NDT;  // latent padded to whole 16-wide tiles
+  static constexpr int CH = DP / 4;    // 8-B chunks per dU image row
+  // bf16 images, 3 planes each (uint16_t units)
+  static constexpr int LDW = H1;       // W8 image row: 64 B, chunk-swizzled (swz_w)
+  static constexpr int PW = DP * LDW;  // one plane of a W8 image [DP][LDW]
+  static constexpr int PA1 = R * H1;   // one plane of the A1 image [R][32] (chunk-swizzled)
+  static constexpr int PU = R * DP;    // one plane of the dU image [R][DP] (chunk-swizzled)
+  static constexpr int W8own = 0;
+  static constexpr int A1i = W8own + 3 * PW;
+  static constexpr int dUi = A1i + 3 * PA1;
+  static constexpr int W8oth = dUi;  // the other tower's W8 lives in the dU region during the forward
+  static constexpr int hend = dUi + 3 * PU;
+  // fp32 region (float units)
+  static constexpr int rsc = (dUi + 3 * PW) / 2;  // [4R] replica-sum scratch (phase 0), dU region after W8oth
+  static constexpr int b8s = hend / 2;            // [2][DP] b8 of oth | own (0 for d >= D)
+  static constexpr int cf1 = b8s + 2 * DP;        // [2][4][H1] BN1 mean | gamma*inv | beta | inv per tower
+  static constexpr int red = cf1 + 8 * H1;        // [2*H1] dgamma1 | dbeta1 block partials
+  static constexpr int scal = red + 2 * H1;       // [0] loss part [1] dls part
+  static constexpr int rst = scal + 4;            // [2][2*H1] BN1 moment sums S1|S2 per tower
+  static constexpr int total = rst + 4 * H1;      // floats
+  static_assert(3 * PW + 8 * R <= 3 * PU, "W8oth + rsc inside the dU region");
+  static_assert(A1i % 8 == 0 && dUi % 8 == 0 && hend % 8 == 0, "16-B aligned images");
 };
+
+// LDS image swizzles: 8-B chunk c of image row rr is stored at chunk
+// c ^ swz(rr) (XOR of row bits; stores bank by dword mod 32, reads mod 64).
+// dU image (256-B rows): bits 0-3 of swz_u a bijection of rr's bits 0-3, so
+// the 8-B accumulator-layout stores (16 rows x 1 chunk per 16-lane group) are
+// conflict-free; bits 2-4 a bijection of rr's bits 0, 1, 3, so the transposed
+// reads (8 rows x 4 consecutive chunks per half wave) are conflict-free.
+template <int CH>
+__device__ __forceinline__ int swz_u(int rr) {
+  const int b0 = rr & 1, b1 = (rr >> 1) & 1, b2 = (rr >> 2) & 1, b3 = (rr >> 3) & 1;
+  return (b3 | (b2 << 1) | (b0 << 2) | (b1 << 3) | (b3 << 4)) & (CH - 1);
+}
+// A1 image (64-B rows, 16-B stores = chunk pairs, so the XOR is even):
+// conflict-free stores and transposed reads
+__device__ __forceinline__ int swz_a(int rr) {
+  return (((rr >> 1) & 1) << 1) | ((((rr >> 2) ^ (rr >> 3)) & 1) << 2);
+}
+// W8 image (64-B rows): conflict-free 16-B forward reads, 2-way transposed reads
+__device__ __forceinline__ int swz_w(int d) { return ((d >> 2) & 1) << 2; }
+
+// 4 floats -> 4 bf16 in each of the 3 planes (8-B stores)
+__device__ __forceinline__ void put_planes4(uint16_t* dst, int plane, const float4& v) {
+  uint32_t h01, m01, l01, h23, m23, l23;
+  split3x2(v.x, v.y, h01, m01, l01);
+  split3x2(v.z, v.w, h23, m23, l23);
+  *reinterpret_cast<u32x2*>(dst) = (u32x2){h01, h23};
+  *reinterpret_cast<u32x2*>(dst + plane) = (u32x2){m01, m23};
+  *reinterpret_cast<u32x2*>(dst + 2 * plane) = (u32x2){l01, l23};
+}
 
 template <int NDT, int R>
 __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   using L = TopLds<NDT, R>;
-  constexpr int NTH = R * 4;
-  constexpr int ZPT = R * (H1 / 4) / NTH;                // float4 of Z4 per thread (2)
-  constexpr int WPT = (L::DP * H1 / 4 + NTH - 1) / NTH;  // float4 of W8 per thread
+  constexpr int NTH = R * 4, NW = R / 16, DP = L::DP;
+  constexpr int WF4 = DP * (H1 / 4);  // float4 of one tower's padded W8
+  constexpr int WPT = (WF4 + NTH - 1) / NTH;
+  static_assert(NDT % 2 == 0, "a dA1 K step pairs two latent tiles");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
   const bool bwd = a.mode != TOP_FWD;
   const int own = bwd ? (int)blockIdx.y : 0;
   const int oth = 1 - own;
@@ -480,20 +581,20 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   const int D = a.D;
-  float* W8s = smem + L::W8s;
-  float* A1s = smem + L::A1s;
-  float* Z4s = smem + L::Z4s;
+  const int rl = 16 * w + r;  // this lane's row in the tile (all 4 lane groups)
+  const int64_t row = r0 + rl;
   TT_STAMP(2, 0);
 
-  // ---- phase 0: issue every load: both towers' Z4 tile and W8, biases,
-  // logit_scale, per-row (target, weight) or dscore
-  float4 zo[ZPT], zs[ZPT], wo[WPT], ws[WPT];
-#pragma unroll
-  for (int k = 0; k < ZPT; ++k) {
-    const int e = threadIdx.x + k * NTH;
-    const int rl = e >> 3, c4 = (e & 7) * 4;
-    zo[k] = *reinterpret_cast<const float4*>(a.tw[oth].Z4 + (r0 + rl) * H1 + c4);
-    zs[k] = *reinterpret_cast<const float4*>(a.tw[own].Z4 + (r0 + rl) * H1 + c4);
+  // ---- phase 0: issue every load: both towers' Z4 slices and W8, biases,
+  // logit_scale, this row's (target, weight) or dscore
+  float4 zo[2], zs[2], wo[WPT], ws[WPT];
+  {
+    const float4* po = reinterpret_cast<const float4*>(a.tw[oth].Z4 + row * H1 + 8 * g);
+    const float4* ps = reinterpret_cast<const float4*>(a.tw[own].Z4 + row * H1 + 8 * g);
+    zo[0] = po[0];
+    zo[1] = po[1];
+    zs[0] = ps[0];
+    zs[1] = ps[1];
   }
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
@@ -501,32 +602,42 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     wo[k] = reinterpret_cast<const float4*>(a.tw[oth].W8)[e];
     ws[k] = reinterpret_cast<const float4*>(a.tw[own].W8)[e];
   }
-  float bo[NDT], bs[NDT];
-#pragma unroll
-  for (int j = 0; j < NDT; ++j) {
-    const int d = min(16 * j + r, D - 1);
-    bo[j] = a.tw[oth].b8[d];
-    bs[j] = a.tw[own].b8[d];
+  float bo = 0.f, bs = 0.f;
+  if (threadIdx.x < DP) {
+    const int d = min((int)threadIdx.x, D - 1);
+    bo = a.tw[oth].b8[d];
+    bs = a.tw[own].b8[d];
   }
   const float lsc = *a.logit_scale;
-  float tg[4], wt[4];
+  float tg = 0.f, wt = 0.f;
+  if (a.mode == TOP_TRAIN) {
+    const float2 v = *reinterpret_cast<const float2*>(a.tgw + 2 * row);
+    tg = v.x;
+    wt = v.y;
+  } else if (a.mode == TOP_BWD_GIVEN) {
+    tg = a.dscore[min(row, a.B - 1)];
+  }
+  RepSum2<NTH, 2 * H1> rs;
+  if (a.train) rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
+  // while the replica loads are in flight: biases, zeroed partials, W8 images
+  if (threadIdx.x < DP) {
+    const bool ok = (int)threadIdx.x < D;
+    smem[L::b8s + threadIdx.x] = ok ? bo : 0.f;
+    smem[L::b8s + DP + threadIdx.x] = ok ? bs : 0.f;
+  }
+  if (threadIdx.x < 2 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;  // red + scal
+  // W8 images: 3 bf16 planes of [DP][LDW], rows d >= D zero
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t row = r0 + 16 * w + 4 * g + i;
-    tg[i] = 0.f;
-    wt[i] = 0.f;
-    if (a.mode == TOP_TRAIN) {
-      const float2 v = *reinterpret_cast<const float2*>(a.tgw + 2 * row);
-      tg[i] = v.x;
-      wt[i] = v.y;
-    } else if (a.mode == TOP_BWD_GIVEN) {
-      tg[i] = a.dscore[min(row, a.B - 1)];
+  for (int k = 0; k < WPT; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    if (e < WF4) {
+      const int d = e >> 3, c = ((e & 7) ^ swz_w(d)) * 4;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      put_planes4(hs + L::W8oth + d * L::LDW + c, L::PW, d < D ? wo[k] : z);
+      put_planes4(hs + L::W8own + d * L::LDW + c, L::PW, d < D ? ws[k] : z);
     }
   }
-  if (a.train) {
-    rep_sum<NTH, 2 * H1>(a.tw[0].st1, 2 * H1, smem + L::rsc, smem + L::rst);
-    rep_sum<NTH, 2 * H1>(a.tw[1].st1, 2 * H1, smem + L::rsc, smem + L::rst + 2 * H1);
-  }
+  if (a.train) rs.finish(smem + L::rsc, smem + L::rst);
   if (threadIdx.x < 2 * H1) {
     const int tau = threadIdx.x / H1, c = threadIdx.x % H1;
     const TowerDev& T = a.tw[tau];
@@ -539,195 +650,231 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     cf[2 * H1 + c] = T.be1[c];
     cf[3 * H1 + c] = inv;
   }
-  if (threadIdx.x < L::DP) smem[L::db8 + threadIdx.x] = 0.f;
-  if (threadIdx.x < 2 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;  // red + scal
   __syncthreads();
   TT_STAMP(2, 1);
 
+  // ---- this lane's A1 slice (row rl, hidden 8g..8g+7) of both towers:
+  // BN1 + ReLU + dropout of Z4, split into bf16 planes (the forward's B operand)
   const bool drop = a.train && a.drop_thr > 0;
-  // write one tower's A1 (and optionally raw Z4) + W8 into LDS
-  auto put = [&](int tau, const float4(&zz)[ZPT], const float4(&ww)[WPT], bool keep_z) {
-    const float* cf = smem + L::cf1 + tau * 4 * H1;
-    const uint64_t key = dropout_key(a.seed, (uint64_t)step, tau, 1);
+  float a1s[8], z4s[8];
+  bf16x8 po[3], ps[3];
+  {
+    auto act = [&](int tau, const float4 (&z)[2], float (&y)[8]) {
+      const f32x4* cf = reinterpret_cast<const f32x4*>(smem + L::cf1 + tau * 4 * H1 + 8 * g);
+      const f32x4 mu[2] = {cf[0], cf[1]}, al[2] = {cf[H1 / 4], cf[H1 / 4 + 1]}, be[2] = {cf[H1 / 2], cf[H1 / 2 + 1]};
+      const float zz[8] = {z[0].x, z[0].y, z[0].z, z[0].w, z[1].x, z[1].y, z[1].z, z[1].w};
 #pragma unroll
-    for (int k = 0; k < ZPT; ++k) {
-      const int e = threadIdx.x + k * NTH;
-      const int rl = e >> 3, c4 = (e & 7) * 4;
-      const uint64_t ctr = (uint64_t)(r0 + rl) * H1 + c4;
-      float4 o;
-      o.x = bn_relu_drop(zz[k].x, cf[c4 + 0], cf[H1 + c4 + 0], cf[2 * H1 + c4 + 0], drop, key, ctr + 0, a.drop_thr, a.drop_scale);
-      o.y = bn_relu_drop(zz[k].y, cf[c4 + 1], cf[H1 + c4 + 1], cf[2 * H1 + c4 + 1], drop, key, ctr + 1, a.drop_thr, a.drop_scale);
-      o.z = bn_relu_drop(zz[k].z, cf[c4 + 2], cf[H1 + c4 + 2], cf[2 * H1 + c4 + 2], drop, key, ctr + 2, a.drop_thr, a.drop_scale);
-      o.w = bn_relu_drop(zz[k].w, cf[c4 + 3], cf[H1 + c4 + 3], cf[2 * H1 + c4 + 3], drop, key, ctr + 3, a.drop_thr, a.drop_scale);
-      *reinterpret_cast<float4*>(A1s + rl * L::LDA + c4) = o;
-      if (keep_z) *reinterpret_cast<float4*>(Z4s + rl * L::LDA + c4) = zz[k];
-    }
-#pragma unroll
-    for (int k = 0; k < WPT; ++k) {
-      const int e = threadIdx.x + k * NTH;
-      if (e < L::DP * (H1 / 4)) {
-        const int d = e >> 3, c4 = (e & 7) * 4;
-        const float4 v = d < D ? ww[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(W8s + d * L::LDA + c4) = v;
+      for (int e = 0; e < 8; ++e) {
+        const float v = (zz[e] - mu[e >> 2][e & 3]) * al[e >> 2][e & 3] + be[e >> 2][e & 3];
+        y[e] = v > 0.f ? v : 0.f;
       }
-    }
-  };
-  auto gemm = [&](const float(&bias)[NDT], f32x4(&acc)[NDT]) {
+#ifdef EXP_NODROP
+      if (false) {
+#else
+      if (drop) {
+#endif
+        const uint64_t key = dropout_key(a.seed, (uint64_t)step, tau, 1);
+        const uint32_t rk = dropout_row_key(key, row);
 #pragma unroll
-    for (int j = 0; j < NDT; ++j) acc[j] = zero4();
-    strip_gemm_nt<NDT>(A1s + 16 * w * L::LDA, L::LDA, W8s, L::LDA, H1, acc);
+        for (int e = 0; e < 8; ++e) y[e] = dropout_keep_rk(rk, 8 * g + e, a.drop_thr) ? y[e] * a.drop_scale : 0.f;
+      }
+    };
+    float a1o[8];
+    act(oth, zo, a1o);
+    act(own, zs, a1s);
+    split8x3(a1o, po);
+    split8x3(a1s, ps);
+    const float zz[8] = {zs[0].x, zs[0].y, zs[0].z, zs[0].w, zs[1].x, zs[1].y, zs[1].z, zs[1].w};
 #pragma unroll
-    for (int j = 0; j < NDT; ++j) acc[j] += (16 * j + r < D) ? bias[j] : 0.f;
-  };
+    for (int e = 0; e < 8; ++e) z4s[e] = zz[e];
+  }
+  if (bwd) {  // own A1 image (16-B chunk pair 2g, swizzled)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      *reinterpret_cast<bf16x8*>(hs + L::A1i + p * L::PA1 + rl * H1 + ((2 * g) ^ swz_a(rl)) * 4) = ps[p];
+  }
 
-  f32x4 accO[NDT], accS[NDT];
-  put(oth, zo, wo, false);
-  __syncthreads();
   TT_STAMP(2, 2);
-  gemm(bo, accO);
-  __syncthreads();
-  TT_STAMP(2, 3);
-  put(own, zs, ws, bwd);
-  __syncthreads();
-  TT_STAMP(2, 4);
-  gemm(bs, accS);
-
-  // ---- cosine (symmetric in own/other: no runtime choice of register arrays)
-  const float s = expf(lsc);
-  float ino[4], int_[4], cs[4], ds[4], sc[4];
-  bool valid[4];
-  float loss_p = 0.f, dls_p = 0.f;
-  const float inv_b = 1.f / (float)a.B;
+  // ---- forward, transposed: lane (r, g) gets U[row rl][16j + 4g + i]
+  f32x4 accO[NDT], accS[NDT];
+  {
+    // W8 fragments of latent tile j+1 are in flight during tile j's MFMAs
+    auto ld = [&](int j, bf16x8 (&fo)[3], bf16x8 (&fs)[3]) {
+      const int dr = 16 * j + r;
+      const int off = dr * L::LDW + ((2 * g) ^ swz_w(dr)) * 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float uv = 0.f, oo = 0.f, tt2 = 0.f;
+      for (int p = 0; p < 3; ++p) {
+        fo[p] = *reinterpret_cast<const bf16x8*>(hs + L::W8oth + p * L::PW + off);
+        fs[p] = *reinterpret_cast<const bf16x8*>(hs + L::W8own + p * L::PW + off);
+      }
+    };
+    bf16x8 fo[2][3], fs[2][3];
+    ld(0, fo[0], fs[0]);
 #pragma unroll
     for (int j = 0; j < NDT; ++j) {
+      if (j + 1 < NDT) ld(j + 1, fo[(j + 1) & 1], fs[(j + 1) & 1]);
+      accO[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + 16 * j + 4 * g);  // bias first: U = b + sum
+      accS[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + DP + 16 * j + 4 * g);
+#ifndef EXP_NOFWD
+      mfma_x3(fo[j & 1], po, accO[j]);
+      mfma_x3(fs[j & 1], ps, accS[j]);
+#else
+      accO[j] += fo[j & 1][0][0] + fo[j&1][1][1] + fo[j&1][2][2]; accS[j] += fs[j & 1][0][0] + po[0][1] + ps[1][0];
+#endif
+    }
+  }
+  if (bwd) __syncthreads();  // W8oth (dU region) read by every wave; A1 image complete
+  TT_STAMP(2, 3);
+
+  // ---- cosine, one row per lane
+  const float s = expf(lsc);
+  float uv = 0.f, oo = 0.f, tt2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < NDT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
       uv += accS[j][i] * accO[j][i];
       oo += accS[j][i] * accS[j][i];
       tt2 += accO[j][i] * accO[j][i];
     }
-    uv = row_reduce16(uv);
-    oo = row_reduce16(oo);
-    tt2 = row_reduce16(tt2);
-    ino[i] = __builtin_amdgcn_rsqf(oo);  // v_rsq_f32 (1 ulp): no IEEE divides
-    int_[i] = __builtin_amdgcn_rsqf(tt2);
-    cs[i] = uv * ino[i] * int_[i];
-    sc[i] = cs[i] * s;
-    const int64_t row = r0 + 16 * w + 4 * g + i;
-    valid[i] = row < a.B;
-    float dsi = 0.f;
-    if (a.mode == TOP_TRAIN) {
-      const float diff = sc[i] - tg[i];
-      dsi = 2.f * diff * (wt[i] * inv_b);
-      loss_p += valid[i] ? wt[i] * diff * diff : 0.f;
-    } else if (a.mode == TOP_BWD_GIVEN) {
-      dsi = tg[i];
-    }
-    ds[i] = valid[i] ? dsi : 0.f;
-    dls_p += ds[i] * sc[i];
+  uv = col_reduce(uv);
+  oo = col_reduce(oo);
+  tt2 = col_reduce(tt2);
+  const float ino = __builtin_amdgcn_rsqf(oo);  // v_rsq_f32 (1 ulp): no IEEE divides
+  const float int_ = __builtin_amdgcn_rsqf(tt2);
+  const float cs = uv * ino * int_;
+  const float sc = cs * s;
+  const bool valid = row < a.B;
+  float ds = 0.f, loss_p = 0.f;
+  if (a.mode == TOP_TRAIN) {
+    const float diff = sc - tg;
+    ds = 2.f * diff * (wt * (1.f / (float)a.B));
+    loss_p = valid ? wt * diff * diff : 0.f;
+  } else if (a.mode == TOP_BWD_GIVEN) {
+    ds = tg;
   }
-  if (a.score && own == 0 && r == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t row = r0 + 16 * w + 4 * g + i;
-      if (row < a.B) a.score[row] = sc[i];
-    }
-  }
+  ds = valid ? ds : 0.f;
+  if (a.score && own == 0 && g == 0 && valid) a.score[row] = sc;
   if (!bwd) return;
 
-  if (own == 0) {  // loss + logit_scale grad once per row tile
-    // every lane of a row group holds the same loss_p / dls_p: sum over g
-    const float lp = col_reduce(loss_p), dp = col_reduce(dls_p);
+  if (own == 0) {  // loss + logit_scale grad once per row tile (lane group 0 covers the rows)
+    const float lp = row_reduce16(loss_p), dp = row_reduce16(ds * sc);
     if (l == 0) {
       atomicAdd(smem + L::scal + 0, lp);
       atomicAdd(smem + L::scal + 1, dp);
     }
   }
 
-  // own-tower output gradient in C layout (SURVEY 3D closed form),
-  // d(own) = dc * (oth/|oth| - own * cos/|own|) / |own|
-  f32x4 dO[NDT];
+  // ---- own-tower output gradient (SURVEY 3D closed form)
+  //   dU = dc (oth/|oth| - own cos/|own|) / |own|,
+  // split into planes per K step t (latent tiles 2t, 2t+1): stored into the
+  // dU image for dW8 and used at once as the B operand of dA1^T
+  const float dc = ds * s;
+  const float ka = valid ? dc * ino * int_ : 0.f;
+  const float kb = valid ? dc * cs * ino * ino : 0.f;
+  const int qd = (l & 15) >> 2, pc = l & 3;  // transposed read: row q, chunk p of this lane
+  const int su = swz_u<L::CH>(rl);
+  uint16_t* dUs = hs + L::dUi;
+  f32x4 dA[2] = {zero4(), zero4()};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float dc = ds[i] * s;
-    const float ka = valid[i] ? dc * ino[i] * int_[i] : 0.f;
-    const float kb = valid[i] ? dc * cs[i] * ino[i] * ino[i] : 0.f;
-#pragma unroll
-    for (int j = 0; j < NDT; ++j) dO[j][i] = ka * accO[j][i] - kb * accS[j][i];
-  }
-
-  const TowerDev& T = a.tw[own];
-  float* A1T = smem + L::A1T;
-  float* dUT = smem + L::dUT;
-  const float* cf = smem + L::cf1 + own * 4 * H1;
-  f32x4 a1[2], z4[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int t = 0; t < NDT / 2; ++t) {
+    float x[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      a1[q][i] = A1s[(16 * w + 4 * g + i) * L::LDA + 16 * q + r];
-      z4[q][i] = Z4s[(16 * w + 4 * g + i) * L::LDA + 16 * q + r];
+      x[i] = ka * accO[2 * t][i] - kb * accS[2 * t][i];
+      x[4 + i] = ka * accO[2 * t + 1][i] - kb * accS[2 * t + 1][i];
     }
-    store_tile_T(A1T, L::LDT, 16 * q, 16 * w, a1[q]);
-  }
-  // transposed dU image (one ds_write_b128 per tile) + db8 column sums
+    bf16x8 du[3];
+    split8x3(x, du);
 #pragma unroll
-  for (int j = 0; j < NDT; ++j) {
-    store_tile_T(dUT, L::LDT, 16 * j, 16 * w, dO[j]);
-    const float cb = col_reduce(dO[j][0] + dO[j][1] + dO[j][2] + dO[j][3]);
-    if (g == 0) atomicAdd(smem + L::db8 + 16 * j + r, cb);
+    for (int p = 0; p < 3; ++p) {
+      const u32x4 v = __builtin_bit_cast(u32x4, du[p]);
+      uint16_t* base = dUs + p * L::PU + rl * DP;
+      *reinterpret_cast<u32x2*>(base + ((8 * t + g) ^ su) * 4) = (u32x2){v[0], v[1]};
+      *reinterpret_cast<u32x2*>(base + ((8 * t + 4 + g) ^ su) * 4) = (u32x2){v[2], v[3]};
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      bf16x8 wf[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int d0 = 32 * t + 4 * g + qd, d1 = d0 + 16;
+        const uint16_t* b = hs + L::W8own + p * L::PW;
+        wf[p] = tr_frag(b + d0 * L::LDW + ((2 * pc + q) ^ swz_w(d0)) * 4, b + d1 * L::LDW + ((2 * pc + q) ^ swz_w(d1)) * 4);
+      }
+      mfma_x3(wf, du, dA[q]);
+    }
   }
-  __syncthreads();
+  TT_STAMP(2, 4);
+
+  // ---- dY1 = dA1 * mask * scale (mask = [A1 > 0] covers ReLU and dropout),
+  // dgamma1 / dbeta1 partials
+  const TowerDev& T = a.tw[own];
+  const float* cf = smem + L::cf1 + own * 4 * H1;
+  const float scl = (a.drop_thr > 0) ? a.drop_scale : 1.f;
+  float dy[8], sg[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int h = 8 * g + e;
+    dy[e] = a1s[e] > 0.f ? dA[e >> 2][e & 3] * scl : 0.f;  // 0 on rows >= B (dU = 0)
+    sg[e] = dy[e] * ((z4s[e] - cf[h]) * cf[3 * H1 + h]);
+  }
+  {
+    float4* py = reinterpret_cast<float4*>(T.dY1 + row * H1 + 8 * g);
+    py[0] = make_float4(dy[0], dy[1], dy[2], dy[3]);
+    py[1] = make_float4(dy[4], dy[5], dy[6], dy[7]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float vg = row_reduce16(sg[e]), vb = row_reduce16(dy[e]);
+    if (r == 0) {
+      atomicAdd(smem + L::red + 8 * g + e, vg);
+      atomicAdd(smem + L::red + H1 + 8 * g + e, vb);
+    }
+  }
+  __syncthreads();  // dU image, BN partials
   TT_STAMP(2, 5);
 
-  // dW8 = dU^T A1 over all R rows of the tile: each wave owns whole output
-  // tiles (no cross-wave reduction) and stores them into this tile's slab
-  // (rows d >= D of dU are zero: the padded slab rows are never read).
+  // ---- dW8 (as dW8^T[h][d]) and db8 over the R rows of the tile: wave w owns
+  // latent tiles w, w + NW, ...; K = rows, 32 per step, read transposed
   float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
-  for (int p = w; p < NDT; p += R / 16) {
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  for (int pt = w; pt < NDT; pt += NW) {
     f32x4 acc[2] = {zero4(), zero4()};
-    strip_gemm_nt<2>(dUT + 16 * p * L::LDT, L::LDT, A1T, L::LDT, R, acc);
-    if (16 * p + 16 <= D) {
+    f32x4 accb = zero4();
+    // operands of K step kk+1 are read while step kk's MFMAs run
+    auto ld = [&](int kk, bf16x8 (&bu)[3], bf16x8 (&aa)[2][3]) {
+      const int ra = 32 * kk + 8 * g + qd, rb = ra + 4;
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int p = 0; p < 3; ++p) {
+        const uint16_t* u = dUs + p * L::PU;
+        bu[p] = tr_frag(u + ra * DP + ((4 * pt + pc) ^ swz_u<L::CH>(ra)) * 4,
+                        u + rb * DP + ((4 * pt + pc) ^ swz_u<L::CH>(rb)) * 4);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) slab[T.so_W8 + (16 * p + 4 * g + i) * H1 + 16 * q + r] = acc[q][i];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int d = 16 * p + 4 * g + i;
-          if (d < D) slab[T.so_W8 + d * H1 + 16 * q + r] = acc[q][i];
+        for (int q = 0; q < 2; ++q) {
+          const uint16_t* v = hs + L::A1i + p * L::PA1;
+          aa[q][p] = tr_frag(v + ra * H1 + ((4 * q + pc) ^ swz_a(ra)) * 4, v + rb * H1 + ((4 * q + pc) ^ swz_a(rb)) * 4);
         }
+      }
+    };
+    bf16x8 bu[2][3], aa[2][2][3];
+    ld(0, bu[0], aa[0]);
+#pragma unroll
+    for (int kk = 0; kk < R / 32; ++kk) {
+      if (kk + 1 < R / 32) ld(kk + 1, bu[(kk + 1) & 1], aa[(kk + 1) & 1]);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) mfma_x3(aa[kk & 1][q], bu[kk & 1], acc[q]);
+#pragma unroll
+      for (int p = 2; p >= 0; --p) accb = mfma_bf16(ones, bu[kk & 1][p], accb);
+    }
+    // lane (r, g): dW8[d = 16 pt + r][16 q + 4g + i], db8[d] in every element of accb
+    const int d = 16 * pt + r;
+    if (d < D) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) *reinterpret_cast<f32x4*>(slab + T.so_W8 + d * H1 + 16 * q + 4 * g) = acc[q];
+      if (g == 0) slab[T.so_b8 + d] = accb[0];
     }
   }
-
-  // dA1 = dU W8  (A from the transposed dU image, W8s row-major [d][k])
-  f32x4 dA[2] = {zero4(), zero4()};
-  strip_gemm_tn<2>(dUT + 16 * w, L::LDT, W8s, L::LDA, L::DP, dA);
-
-  // dY1 = dA1 * mask*scale * [Y1 > 0]  ==  [A1 > 0] * dA1 * scale
-  const float scl = (a.drop_thr > 0) ? a.drop_scale : 1.f;
-  float sg[2], sb[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int col = 16 * q + r;
-    const float mean = cf[col], inv = cf[3 * H1 + col];
-    sg[q] = 0.f;
-    sb[q] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float dy = a1[q][i] > 0.f ? dA[q][i] * scl : 0.f;  // 0 on rows >= B (dU = 0)
-      T.dY1[(r0 + 16 * w + 4 * g + i) * H1 + col] = dy;
-      sg[q] += dy * ((z4[q][i] - mean) * inv);
-      sb[q] += dy;
-    }
-  }
-  cols_to_lds<2>(sg, smem + L::red);
-  cols_to_lds<2>(sb, smem + L::red + H1);
-  __syncthreads();
   TT_STAMP(2, 6);
 
   if (threadIdx.x < H1) {
@@ -739,7 +886,6 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     atomicAdd(lr, smem[L::scal + 1]);
     if (a.mode == TOP_TRAIN) atomicAdd(lr + 1, smem[L::scal + 0] / (float)a.B);
   }
-  if (threadIdx.x < D) slab[T.so_b8 + threadIdx.x] = smem[L::db8 + threadIdx.x];
   TT_STAMP(2, 7);
 }
 
@@ -834,6 +980,9 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   const bool drop = a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
   f32x4 a0[4], zh0[4];
+  uint32_t rk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) rk[i] = dropout_row_key(key, r0 + 16 * w + 4 * g + i);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = 16 * j + r;
@@ -842,8 +991,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
       const int64_t row = r0 + 16 * w + 4 * g + i;
       const float z = zz0[j][i];
       const bool ok = row < a.B;
-      const float av = bn_relu_drop(z, c0[col], c0[H0 + col], c0[2 * H0 + col], drop, key,
-                                    (uint64_t)row * H0 + col, a.drop_thr, a.drop_scale);
+      const float av = bn_relu_drop(z, c0[col], c0[H0 + col], c0[2 * H0 + col], drop, rk[i], col, a.drop_thr,
+                                    a.drop_scale);
       a0[j][i] = ok ? av : 0.f;
       zh0[j][i] = ok ? (z - c0[col]) * c0[3 * H0 + col] : 0.f;
     }

@@ -29,7 +29,7 @@ itself (``tests/golden/make_golden.py``); ``tests/test_oracle_golden.py``
 checks this restatement against every one of them.  Dropout masks are either
 injected (fixtures made with explicit masks) or regenerated with
 :func:`dropout_keep_mask`, a restatement of the HIP kernels' counter-based RNG
-(``ceo-recommender_amd/csrc/tt_common.h: tt_dropout_keep``).
+(``ceo-recommender_amd/csrc/tt_common.h: dropout_keep``).
 """
 from __future__ import annotations
 
@@ -76,7 +76,7 @@ def buffer_names() -> List[str]:
 
 
 # --------------------------------------------------------------------------
-# dropout RNG restatement (HIP kernels: tt_common.h tt_dropout_keep)
+# dropout RNG restatement (HIP kernels: tt_common.h dropout_key / dropout_keep)
 # --------------------------------------------------------------------------
 _M64 = (1 << 64) - 1
 
@@ -88,6 +88,18 @@ def _mix64(z: np.ndarray) -> np.ndarray:
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
     return z
+
+
+def _perm32(x: np.ndarray) -> np.ndarray:
+    """lowbias32 (tt_common.h perm32) on uint32 arrays (wrapping multiplies)."""
+    x = x.astype(np.uint32)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7FEB352D)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846CA68B)
+        x = x ^ (x >> np.uint32(16))
+    return x
 
 
 def dropout_key(seed: int, step: int, tower: int, layer: int) -> int:
@@ -102,13 +114,16 @@ def dropout_keep_mask(seed: int, step: int, tower: int, layer: int,
     """bool[n_rows, width]: True where the element is kept (prob 1-p)."""
     if p <= 0.0:
         return np.ones((n_rows, width), dtype=bool)
-    key = np.uint64(dropout_key(seed, step, tower, layer))
-    ctr = np.arange(n_rows * width, dtype=np.uint64)
+    key = dropout_key(seed, step, tower, layer)
+    k_lo, k_hi = np.uint32(key & 0xFFFFFFFF), np.uint32(key >> 32)
+    rows = (np.arange(n_rows, dtype=np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    cols = np.arange(width, dtype=np.uint32)
     with np.errstate(over="ignore"):
-        z = key + ctr * np.uint64(0x9E3779B97F4A7C15)
-    h = (_mix64(z) >> np.uint64(40)).astype(np.int64)  # 24 random bits
+        rk = _perm32(rows ^ k_lo) + k_hi                      # per-row key
+        h = _perm32(rk[:, None] ^ (cols[None, :] * np.uint32(0x9E3779B9)))
+    h = (h >> np.uint32(8)).astype(np.int64)  # 24 random bits
     thr = int(p * 16777216.0)
-    return (h >= thr).reshape(n_rows, width)
+    return h >= thr
 
 
 # --------------------------------------------------------------------------

@@ -668,11 +668,7 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
         const float v = (zz[e] - mu[e >> 2][e & 3]) * al[e >> 2][e & 3] + be[e >> 2][e & 3];
         y[e] = v > 0.f ? v : 0.f;
       }
-#ifdef EXP_NODROP
-      if (false) {
-#else
       if (drop) {
-#endif
         const uint64_t key = dropout_key(a.seed, (uint64_t)step, tau, 1);
         const uint32_t rk = dropout_row_key(key, row);
 #pragma unroll
@@ -715,12 +711,8 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
       if (j + 1 < NDT) ld(j + 1, fo[(j + 1) & 1], fs[(j + 1) & 1]);
       accO[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + 16 * j + 4 * g);  // bias first: U = b + sum
       accS[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + DP + 16 * j + 4 * g);
-#ifndef EXP_NOFWD
       mfma_x3(fo[j & 1], po, accO[j]);
       mfma_x3(fs[j & 1], ps, accS[j]);
-#else
-      accO[j] += fo[j & 1][0][0] + fo[j&1][1][1] + fo[j&1][2][2]; accS[j] += fs[j & 1][0][0] + po[0][1] + ps[1][0];
-#endif
     }
   }
   if (bwd) __syncthreads();  // W8oth (dU region) read by every wave; A1 image complete

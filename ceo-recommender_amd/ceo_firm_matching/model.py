@@ -18,6 +18,8 @@ Drop-in for the reference ``ceo_firm_matching/model.py:14-89``:
 """
 from __future__ import annotations
 
+import os
+
 import warnings
 from typing import Dict, Optional
 
@@ -201,6 +203,8 @@ class _FusedTwoTower(torch.autograd.Function):
         desc = arena.desc
         ws_bytes = N.workspace_bytes(desc, max(B, 1))
         ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=f_num.device)
+        if _POISON_WS:  # diagnostic: surface reads of workspace the kernels never wrote
+            ws.fill_(float("nan"))
         score = torch.empty(B, dtype=torch.float32, device=f_num.device)
         seed, step = model.next_dropout_stream() if train else (0, 0)
         batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
@@ -235,6 +239,9 @@ class _FusedTwoTower(torch.autograd.Function):
         offs = N.param_offsets(arena.desc)
         grads = [grad[off:off + p.numel()].view_as(p) for _, p, off in model._named_slots(offs)]
         return (None, None, None, None, None, *grads)
+
+
+_POISON_WS = bool(os.environ.get("CEO_TT_POISON_WS"))
 
 
 def _fused_forward(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):

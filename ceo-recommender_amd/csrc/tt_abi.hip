@@ -144,7 +144,11 @@ static std::once_flag g_attr_once;
 static void set_lds_attrs() {
   std::call_once(g_attr_once, [] {
     const int mx = (int)LDS_MAX;
-    const void* ks[] = {(const void*)k_l0_fwd<ROWS>,     (const void*)k_l4_fwd<ROWS>,
+    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true>, (const void*)k_l0_fwd<ROWS, 1, false>,
+                        (const void*)k_l0_fwd<ROWS, 2, true>, (const void*)k_l0_fwd<ROWS, 2, false>,
+                        (const void*)k_l0_fwd<ROWS, 4, true>, (const void*)k_l0_fwd<ROWS, 4, false>,
+                        (const void*)k_l0_fwd<ROWS, 8, true>, (const void*)k_l0_fwd<ROWS, 8, false>,
+                        (const void*)k_l4_fwd<ROWS>,
                         (const void*)k_top<4, 64>,        (const void*)k_top<8, 64>,
                         (const void*)k_top<4, 128>,       (const void*)k_top<8, 128>,
                         (const void*)k_bwd_mid<ROWS>,    (const void*)k_bwd_first<ROWS>};
@@ -367,7 +371,24 @@ static void launch(K kern, dim3 g, dim3 b, size_t lds, hipStream_t s, Evs ev, A.
 }
 
 static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
-  launch(k_l0_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l0, s, ev, a);
+  // instance by the widest tower input (32-wide K steps held in registers)
+  // and whether both towers take the aligned numeric-only gather
+  const int ks = l0_ks(std::max(a.tw[0].kp, a.tw[1].kp));
+  const bool vec = a.tw[0].num_vec && a.tw[1].num_vec;
+  const dim3 grid(P.n_tiles, 2), blk(4 * ROWS);
+#define TT_L0(KS)                                                                   \
+  if (ks == KS) {                                                                   \
+    if (vec)                                                                        \
+      launch(k_l0_fwd<ROWS, KS, true>, grid, blk, P.lds_l0, s, ev, a);             \
+    else                                                                            \
+      launch(k_l0_fwd<ROWS, KS, false>, grid, blk, P.lds_l0, s, ev, a);            \
+    return;                                                                         \
+  }
+  TT_L0(1)
+  TT_L0(2)
+  TT_L0(4)
+  TT_L0(8)
+#undef TT_L0
 }
 static void launch_l4(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
   launch(k_l4_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l4, s, ev, a);

@@ -159,6 +159,16 @@ __device__ __forceinline__ void split8x3(const float (&x)[8], bf16x8 (&pl)[3]) {
   pl[2] = __builtin_bit_cast(bf16x8, l);
 }
 
+// 4 floats -> 4 bf16 in each of the 3 planes (8-B stores)
+__device__ __forceinline__ void put_planes4(uint16_t* dst, int plane, const float4& v) {
+  uint32_t h01, m01, l01, h23, m23, l23;
+  split3x2(v.x, v.y, h01, m01, l01);
+  split3x2(v.z, v.w, h23, m23, l23);
+  *reinterpret_cast<u32x2*>(dst) = (u32x2){h01, h23};
+  *reinterpret_cast<u32x2*>(dst + plane) = (u32x2){m01, m23};
+  *reinterpret_cast<u32x2*>(dst + 2 * plane) = (u32x2){l01, l23};
+}
+
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -344,6 +354,13 @@ __device__ __forceinline__ int64_t batch_row0(const StepArgs& a, int64_t t) {
 // dataset row of batch row i
 __device__ __forceinline__ int64_t data_row(const StepArgs& a, int64_t base, int64_t i) {
   return a.rows ? a.rows[base + i] : base + i;
+}
+// the same without a branch around the load (the load goes to a valid dummy
+// address when there is no permutation): keeps the issue phase straight-line
+__device__ __forceinline__ int64_t data_row_nb(const StepArgs& a, int64_t base, int64_t i) {
+  const int64_t* p = a.rows ? a.rows + (base + i) : reinterpret_cast<const int64_t*>(a.lsr);
+  const int64_t v = *p;
+  return a.rows ? v : base + i;
 }
 
 // ---------------------------------------------------------------------------

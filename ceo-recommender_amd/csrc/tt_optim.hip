@@ -48,6 +48,14 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
   if (e < a.n)
     for (int k = 0; k < a.n_seg; ++k)
       if (e >= a.seg[k].off && e < a.seg[k].off + a.seg[k].len) { si = k; break; }
+  // the Adam state of this element is loaded up front: its latency overlaps the slab loads
+  const bool owner = pg == 0 && si >= 0;
+  float pp = 0.f, pm = 0.f, pv = 0.f;
+  if (owner && a.apply_adam) {
+    pp = a.p[e];
+    pm = a.m[e];
+    pv = a.v[e];
+  }
   float acc = 0.f;
   if (si >= 0) {
     const Seg& S = a.seg[si];
@@ -78,10 +86,17 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
     }
   }
   part[pg][el] = acc;
-  // zero the BN moment sums consumed by this step; fold the loss replicas (one block)
+  // zero the BN moment sums consumed by this step (one element per thread of
+  // the leading blocks); fold the loss replicas (block 0)
+  {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (i >= 0 && i < a.zero_len[b]) a.zero_buf[b][i] = 0.f;
+      i -= a.zero_len[b];
+    }
+  }
   if (blockIdx.x == 0) {
-    for (int b = 0; b < 4; ++b)
-      for (int i = threadIdx.x; i < a.zero_len[b]; i += blockDim.x) a.zero_buf[b][i] = 0.f;
     if (a.lsr && threadIdx.x == 0) {
       float l = 0.f;
       for (int q = 0; q < NREP; ++q) {
@@ -93,7 +108,7 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
   }
   __syncthreads();
   TT_STAMP(5, 1);
-  if (pg != 0 || si < 0) return;
+  if (!owner) return;
   float gsum = 0.f;
 #pragma unroll
   for (int k = 0; k < RED_G; ++k) gsum += part[k][el];
@@ -102,11 +117,10 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
   if (a.apply_adam) {
     const int64_t t = a.state ? a.state->step_cur : a.step_host;
     const AdamCoef c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
-    float p = a.p[e], m = a.m[e], v = a.v[e];
-    adam_elem(p, m, v, gsum, c);
-    a.p[e] = p;
-    a.m[e] = m;
-    a.v[e] = v;
+    adam_elem(pp, pm, pv, gsum, c);
+    a.p[e] = pp;
+    a.m[e] = pm;
+    a.v[e] = pv;
     if (a.state && blockIdx.x == 0 && el == 0) a.state->step_done = t;
   }
 }

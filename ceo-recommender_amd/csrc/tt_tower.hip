@@ -8,7 +8,7 @@
 // weight-gradient partial slabs travel through memory (at B = 16K all of them
 // sit in the 256 MB Infinity Cache).
 //
-//   k_l0_fwd    Z0 = X W0^T + b0 (X gathered: numeric ++ embeddings), BN0 sums
+//   k_l0_fwd    Z0 = X W0^T + b0 (X gathered per lane: numeric ++ embeddings), BN0 sums
 //               model.py:69-71 (embedding gather + concat), :38 (Linear)
 //   k_l4_fwd    A0 = Dropout(ReLU(BN0(Z0))); Z4 = A0 W4^T + b4,       BN1 sums
 //               model.py:39-42
@@ -268,68 +268,143 @@ __device__ __forceinline__ void row_dot(const float* x, const float* W, int ld, 
 // ---------------------------------------------------------------------------
 // k_l0_fwd : Z0 = X W0^T + b0 ; BN0 shifted moment sums ; (target, weight)
 // ---------------------------------------------------------------------------
+// X W0^T on the bf16x3 MFMA core: each lane gathers the 8-column slices of
+// its own row that it supplies as the A operand (no X tile in LDS, no
+// gather -> LDS -> barrier chain); W0 is staged once per block as bf16 planes.
+// Instances: KS = 32-wide K steps (tower inputs up to 32 KS columns, zero
+// padded), VEC = numeric-only towers with 16-B aligned rows.  The issue phase
+// is straight-line code -- every load unconditional at a clamped address,
+// out-of-range values zeroed by selects afterwards -- because a branch around
+// a load makes the compiler drain vmcnt at the join, which serialises the
+// gathers behind one another.
+constexpr int l0_ks(int kp) { return kp <= 32 ? 1 : kp <= 64 ? 2 : kp <= 128 ? 4 : 8; }
 template <int R>
 struct L0Lds {
+  __host__ __device__ static constexpr int ldk(int ks) { return 32 * ks + 16; }  // 32-B pad: conflict-free reads
+  // bf16 planes [3][H0][ldk] | red [2*H0] | shl [H0]
   static size_t bytes(int kp) {
-    return sizeof(float) * ((size_t)(H0 + R) * (kp + 4) + 2 * H0 + H0 + kp + 4 * H0) + sizeof(int64_t) * R;
+    return sizeof(uint16_t) * 3 * (size_t)H0 * ldk(l0_ks(kp)) + sizeof(float) * 3 * H0;
   }
 };
 
-template <int R>
+// 8 consecutive tower-input columns c0..c0+7 of dataset row drow, raw
+// (VEC: two float4 at clamped addresses; zero_x8 masks columns >= n_num)
+template <bool VEC>
+__device__ __forceinline__ void tower_x8(const TowerDev& T, int64_t drow, int c0, float (&x)[8]) {
+  if constexpr (VEC) {
+    const float* src = T.num + drow * T.num_ld;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 v = *reinterpret_cast<const float4*>(src + min(c0 + 4 * h, T.n_num - 4));
+      x[4 * h + 0] = v.x;
+      x[4 * h + 1] = v.y;
+      x[4 * h + 2] = v.z;
+      x[4 * h + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = tower_x(T, drow, c0 + e);
+  }
+}
+template <bool VEC>
+__device__ __forceinline__ void zero_x8(const TowerDev& T, int c0, float (&x)[8]) {
+  if constexpr (VEC) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = c0 + e < T.n_num ? x[e] : 0.f;
+  }
+}
+
+template <int R, int KS, bool VEC>
 __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
   constexpr int NTH = R * 4;
+  constexpr int KC = 32 * KS, LDK = L0Lds<R>::ldk(KS), PL = H0 * LDK;
+  constexpr int C4N = KC / 4, N4 = H0 * C4N, WPT = N4 / NTH;  // W0 float4 per thread
+  static_assert(R == 64 && N4 % NTH == 0, "4 waves x 16 rows");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
   const TowerDev& T = a.tw[t];
   const int64_t step = step_for_first_kernel(a);
   const int64_t base = batch_row0(a, step);
   const int64_t r0 = (int64_t)blockIdx.x * R;
-  const int kp = T.kp, ldk = kp + 4;
+  const int in = T.in_dim;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  int64_t* ridx = reinterpret_cast<int64_t*>(smem);  // [R]
-  float* Ws = smem + 2 * R;        // [64][ldk]
-  float* Xs = Ws + H0 * ldk;       // [R][ldk]
-  float* red = Xs + R * ldk;       // [128]
-  float* shl = red + 2 * H0;       // [64] moment shift = Z0 of batch row 0
-  float* x0 = shl + H0;            // [kp] X of batch row 0
-  float* part = x0 + kp;           // [4][64]
+  uint16_t* Wh = reinterpret_cast<uint16_t*>(smem);
+  float* red = reinterpret_cast<float*>(Wh + 3 * PL);  // [128]
+  float* shl = red + 2 * H0;                           // [64] moment shift = Z0 of batch row 0
   TT_STAMP(0, 0);
 
+  // ---- issue (straight line): row indices; W0 (raw, clamped); this lane's
+  // X slices (A operand: row 16w + r, columns 32kk + 8g .. +7; rows beyond B
+  // gather a duplicate row) and the same slices of the batch's row 0
+  const int64_t dr = data_row_nb(a, base, min(r0 + 16 * w + r, a.B - 1));
+  const int64_t dr0 = data_row_nb(a, base, 0);
+  float4 wv[WPT];
+#pragma unroll
+  for (int k = 0; k < WPT; ++k) {
+    const int e = k * NTH + (int)threadIdx.x;
+    const int h = e / C4N, c = 4 * (e - h * C4N);
+    const float* rw = T.W0 + (int64_t)h * in;
+    if constexpr (VEC)
+      wv[k] = *reinterpret_cast<const float4*>(rw + min(c, in - 4));
+    else
+      wv[k] = make_float4(rw[min(c, in - 1)], rw[min(c + 1, in - 1)], rw[min(c + 2, in - 1)], rw[min(c + 3, in - 1)]);
+  }
+  float xr[KS][8], x0[KS][8];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    tower_x8<VEC>(T, dr, 32 * kk + 8 * g, xr[kk]);
+    tower_x8<VEC>(T, dr0, 32 * kk + 8 * g, x0[kk]);
+  }
   float bias[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = T.b0[16 * j + r];
-  if (a.state && blockIdx.x == 0 && t == 0 && threadIdx.x == 0) a.state->step_cur = step;
-  stage_ridx<R>(a, base, r0, ridx);
+  const float bsh = T.b0[16 * w + r];
   if (threadIdx.x < 2 * H0) red[threadIdx.x] = 0.f;
-  if (a.train) {
-    const int64_t dr0 = data_row(a, base, 0);
-    for (int c = threadIdx.x; c < kp; c += NTH) x0[c] = tower_x(T, dr0, c);
+  // W0 image: zero columns >= in, split, store
+#pragma unroll
+  for (int k = 0; k < WPT; ++k) {
+    const int e = k * NTH + (int)threadIdx.x;
+    const int h = e / C4N, c = 4 * (e - h * C4N);
+    const float4 u = make_float4(c + 0 < in ? wv[k].x : 0.f, c + 1 < in ? wv[k].y : 0.f, c + 2 < in ? wv[k].z : 0.f,
+                                 c + 3 < in ? wv[k].w : 0.f);
+    put_planes4(Wh + h * LDK + c, PL, u);
   }
-  stage_w<NTH>(T.W0, H0, T.in_dim, kp, Ws, ldk);
   __syncthreads();
   TT_STAMP(0, 1);
-  if (t == 0 && a.target && threadIdx.x < R) {  // (target, weight) of the tile's rows for k_top
-    const int64_t dr = ridx[threadIdx.x];
-    const float tv = a.target[dr], wv = a.weight[dr];
-    *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + threadIdx.x)) = make_float2(tv, wv);
-  }
-  stage_x<R, NTH>(T, ridx, Xs, ldk);
-  __syncthreads();
-  TT_STAMP(0, 2);
 
-  if (a.train) {
-    // Shifted moment sums: every block derives the same shift (Z0 of the
-    // batch's first row, identical fp32 ops in every block), which keeps
-    // var = S2/B - (S1/B)^2 free of cancellation for any data offset.
-    row_dot<NTH>(x0, Ws, ldk, T.in_dim, H0, T.b0, part, shl);
-    if (blockIdx.x == 0 && threadIdx.x < H0) T.shift0[threadIdx.x] = shl[threadIdx.x];
-  }
-  f32x4 acc[4];
+  // ---- Z0 = X W0^T (+ b0): lane (r, g) of wave w gets rows 16w + 4g + i,
+  // column 16j + r.  Shift row: wave w computes Z0[row 0] columns 16w..16w+15
+  // with the same MFMA sequence in every block (bitwise one shift for all),
+  // which keeps var = S2/B - (S1/B)^2 free of cancellation for any data offset.
+  f32x4 acc[4], accs = zero4();
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = zero4();
-  strip_gemm_nt<4>(Xs + 16 * w * ldk, ldk, Ws, ldk, kp, acc);
-  __syncthreads();
-  TT_STAMP(0, 3);
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    zero_x8<VEC>(T, 32 * kk + 8 * g, xr[kk]);
+    zero_x8<VEC>(T, 32 * kk + 8 * g, x0[kk]);
+    bf16x8 xa[3], xs[3];
+    split8x3(xr[kk], xa);
+    split8x3(x0[kk], xs);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x8 wf[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        wf[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * j + r) * LDK + 32 * kk + 8 * g);
+      mfma_x3(xa, wf, acc[j]);
+      if (j == w) mfma_x3(xs, wf, accs);
+    }
+  }
+  if (a.train) {
+    if (g == 0) {
+      const float sh = accs[0] + bsh;
+      shl[16 * w + r] = sh;
+      if (blockIdx.x == 0) T.shift0[16 * w + r] = sh;
+    }
+    __syncthreads();  // shl
+  }
+  TT_STAMP(0, 2);
 
   float s1[4], s2[4];
 #pragma unroll
@@ -340,10 +415,10 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
     s2[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int64_t row = r0 + 16 * w + 4 * g + i;
+      const int64_t rw = r0 + 16 * w + 4 * g + i;
       const float z = acc[j][i] + bias[j];
       acc[j][i] = z;
-      const float d = row < a.B ? z - sh : 0.f;
+      const float d = rw < a.B ? z - sh : 0.f;
       s1[j] += d;
       s2[j] += d * d;
     }
@@ -357,11 +432,16 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) T.Z0[(r0 + 16 * w + 4 * g + i) * H0 + 16 * j + r] = acc[j][i];
+  if (t == 0 && a.target && threadIdx.x < R) {  // (target, weight) of the tile's rows for k_top
+    const int64_t drt = data_row(a, base, min(r0 + (int64_t)threadIdx.x, a.B - 1));
+    *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + threadIdx.x)) = make_float2(a.target[drt], a.weight[drt]);
+  }
+  if (a.state && blockIdx.x == 0 && t == 0 && threadIdx.x == 0) a.state->step_cur = step;
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H0) atomicAdd(&T.st0[rep_of_block() * 2 * H0 + threadIdx.x], red[threadIdx.x]);
   }
-  TT_STAMP(0, 4);
+  TT_STAMP(0, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,15 +635,6 @@ __device__ __forceinline__ int swz_a(int rr) {
 // W8 image (64-B rows): conflict-free 16-B forward reads, 2-way transposed reads
 __device__ __forceinline__ int swz_w(int d) { return ((d >> 2) & 1) << 2; }
 
-// 4 floats -> 4 bf16 in each of the 3 planes (8-B stores)
-__device__ __forceinline__ void put_planes4(uint16_t* dst, int plane, const float4& v) {
-  uint32_t h01, m01, l01, h23, m23, l23;
-  split3x2(v.x, v.y, h01, m01, l01);
-  split3x2(v.z, v.w, h23, m23, l23);
-  *reinterpret_cast<u32x2*>(dst) = (u32x2){h01, h23};
-  *reinterpret_cast<u32x2*>(dst + plane) = (u32x2){m01, m23};
-  *reinterpret_cast<u32x2*>(dst + 2 * plane) = (u32x2){l01, l23};
-}
 
 template <int NDT, int R>
 __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
@@ -1239,7 +1310,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   TT_STAMP(4, 3);
 }
 
-template __global__ void k_l0_fwd<64>(StepArgs);
+#define TT_L0(KS) template __global__ void k_l0_fwd<64, KS, true>(StepArgs); \
+  template __global__ void k_l0_fwd<64, KS, false>(StepArgs);
+TT_L0(1)
+TT_L0(2)
+TT_L0(4)
+TT_L0(8)
+#undef TT_L0
 template __global__ void k_l4_fwd<64>(StepArgs);
 template __global__ void k_top<4, 64>(StepArgs);
 template __global__ void k_top<8, 64>(StepArgs);

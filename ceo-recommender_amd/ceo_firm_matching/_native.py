@@ -102,6 +102,9 @@ def lib() -> ctypes.CDLL:
         "tt_nce_backward": (I32, [P, P, I64, I64, I32, I64, I64, F, P, I64, P, P, P]),
         "tt_rank_workspace_bytes": (I64, [I64]),
         "tt_retrieval_ranks": (I32, [P, P, I64, I64, I32, I64, P, I64, P, P]),
+        "tt_triplet_workspace_bytes": (I64, [I64, I64, I32]),
+        "tt_triplet_forward": (I32, [P, P, I64, I64, I32, I64, F, I64, P, I64, P, P, P, P]),
+        "tt_triplet_backward": (I32, [P, P, I64, I64, I32, I64, I64, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

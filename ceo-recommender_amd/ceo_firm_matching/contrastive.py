@@ -46,6 +46,16 @@ def _f32(x: torch.Tensor) -> torch.Tensor:
     return x if x.is_contiguous() else x.contiguous()
 
 
+def _f32_pad4(x: torch.Tensor) -> torch.Tensor:
+    """fp32, contiguous, feature dim zero-padded to a multiple of 4 (the
+    GEMM core stages 4 consecutive k per load; zero columns add nothing to
+    any dot product -- e.g. the default LATENT_DIM 60 gives 30-wide
+    projections)."""
+    x = _f32(x)
+    r = (-x.shape[1]) % 4
+    return F.pad(x, (0, r)) if r else x
+
+
 class _NCE:
     """Host state of one forward (workspace holds E for the backward)."""
 
@@ -93,13 +103,14 @@ class _NCE:
 class _InfoNCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f, c, temperature):
-        f32, c32 = _f32(f), _f32(c)
+        f32, c32 = _f32_pad4(f), _f32_pad4(c)
         B, d = f32.shape
         h = _NCE(f32, c32, B, B, d, 0, B, float(temperature))
         loss, status = h.loss(h.forward(h.norms()))
         _check_status(status)
         ctx.h = h
         ctx.dtypes = (f.dtype, c.dtype)
+        ctx.d_in = f.shape[1]
         return loss.reshape(()).to(f.dtype)
 
     @staticmethod
@@ -107,7 +118,8 @@ class _InfoNCEFn(torch.autograd.Function):
         df, dc = ctx.h.backward()
         ctx.h = None  # release E
         g = g.to(torch.float32)
-        return (df * g).to(ctx.dtypes[0]), (dc * g).to(ctx.dtypes[1]), None
+        d = ctx.d_in
+        return (df[:, :d] * g).to(ctx.dtypes[0]), (dc[:, :d] * g).to(ctx.dtypes[1]), None
 
 
 def info_nce_loss(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, temperature: float = 0.07) -> torch.Tensor:
@@ -129,8 +141,9 @@ class _ShardedNCEFn(torch.autograd.Function):
     def forward(ctx, f, c, temperature, group):
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
-        f32, c32 = _f32(f), _f32(c)
+        f32, c32 = _f32_pad4(f), _f32_pad4(c)
         m, d = f32.shape
+        ctx.d_in = f.shape[1]
         if dist.get_backend(group) == "gloo":
             parts = [torch.empty_like(c32) for _ in range(world)]
             dist.all_gather(parts, c32, group=group)
@@ -164,7 +177,8 @@ class _ShardedNCEFn(torch.autograd.Function):
             dc = torch.empty(m, dc_all.shape[1], dtype=torch.float32, device=dc_all.device)
             dist.reduce_scatter_tensor(dc, dc_all, group=group)
         g = g.to(torch.float32)
-        return df * g, dc * g, None, None
+        d = ctx.d_in
+        return df[:, :d] * g, dc[:, :d] * g, None, None
 
 
 def info_nce_loss_sharded(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, temperature: float = 0.07,
@@ -177,6 +191,79 @@ def info_nce_loss_sharded(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, tempe
     if firm_proj.device.type != "cuda":
         raise NotImplementedError("info_nce_loss_sharded runs on the HIP kernels (one GPU per rank)")
     return _ShardedNCEFn.apply(firm_proj, ceo_proj, temperature, group)
+
+
+# --------------------------------------------------------------------------
+# triplet loss with semi-hard negative mining
+# --------------------------------------------------------------------------
+class _SemiHardFn(torch.autograd.Function):
+    """One fused similarity GEMM + masked-min epilogue (tt_triplet_forward);
+    the backward touches only the mined rows (tt_triplet_backward)."""
+
+    @staticmethod
+    def forward(ctx, f, c, margin):
+        f32, c32 = _f32_pad4(f), _f32_pad4(c)
+        B, d = f32.shape
+        L = N.lib()
+        wsb = int(L.tt_triplet_workspace_bytes(B, B, d))
+        if wsb < 0:
+            N.check(wsb, "tt_triplet_workspace_bytes")
+        ws = torch.empty(wsb // 4, dtype=torch.float32, device=f.device)
+        hardest = torch.empty(B, dtype=torch.int32, device=f.device)
+        row_loss = torch.empty(B, dtype=torch.float32, device=f.device)
+        loss = torch.zeros(1, dtype=torch.float32, device=f.device)
+        st = N.stream_ptr(f.device)
+        N.check(L.tt_triplet_forward(f32.data_ptr(), c32.data_ptr(), B, B, d, 0, ctypes.c_float(margin), B,
+                                     ws.data_ptr(), wsb, hardest.data_ptr(), row_loss.data_ptr(),
+                                     loss.data_ptr(), st), "tt_triplet_forward")
+        ctx.save_for_backward(f32, c32, hardest, row_loss)
+        ctx.meta = (f.dtype, c.dtype, f.shape[1])
+        ctx.mark_non_differentiable(hardest, row_loss)
+        return loss.reshape(()).to(f.dtype), hardest, row_loss
+
+    @staticmethod
+    def backward(ctx, g, _gh, _gr):
+        f32, c32, hardest, row_loss = ctx.saved_tensors
+        B, d = f32.shape
+        g = g.to(torch.float32).reshape(1).contiguous()
+        df = torch.empty_like(f32)
+        dc = torch.empty_like(c32)
+        N.check(N.lib().tt_triplet_backward(f32.data_ptr(), c32.data_ptr(), B, B, d, 0, B, hardest.data_ptr(),
+                                            row_loss.data_ptr(), g.data_ptr(), df.data_ptr(), dc.data_ptr(),
+                                            N.stream_ptr(f32.device)), "tt_triplet_backward")
+        fd, cd, d_in = ctx.meta
+        return df[:, :d_in].to(fd), dc[:, :d_in].to(cd), None
+
+
+def semi_hard_mining(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, margin: float = 0.2):
+    """(loss, hardest column per row, per-row loss) on the HIP kernels."""
+    if firm_proj.device.type != "cuda":
+        raise NotImplementedError("semi_hard_mining runs on the HIP kernels")
+    if firm_proj.shape != ceo_proj.shape or firm_proj.dim() != 2:
+        raise ValueError("semi_hard_negative_mining: firm_proj and ceo_proj must be [B, D] of the same shape")
+    return _SemiHardFn.apply(firm_proj, ceo_proj, float(margin))
+
+
+def semi_hard_negative_mining(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, margin: float = 0.2) -> torch.Tensor:
+    """Triplet loss with semi-hard negative mining (reference
+    contrastive.py:141-192).  dist = 1 - F C^T; per anchor firm i the
+    smallest negative distance in (pos_i, pos_i + margin), else the smallest
+    negative overall; loss = mean_i relu(pos_i - hardest_i + margin).
+    On HIP tensors: one fused GEMM + masked-min kernel instead of the
+    reference's per-row Python loop (ties resolve to the lowest column)."""
+    B = firm_proj.size(0)
+    if B <= 1:
+        return torch.tensor(0.0, device=firm_proj.device)
+    if firm_proj.device.type == "cuda":
+        return semi_hard_mining(firm_proj, ceo_proj, margin)[0]
+    dist_matrix = 1 - torch.mm(firm_proj, ceo_proj.t())
+    pos = torch.diagonal(dist_matrix)
+    eye = torch.eye(B, dtype=torch.bool, device=firm_proj.device)
+    neg = dist_matrix.masked_fill(eye, float("inf"))
+    semi = (neg > pos[:, None]) & (neg < (pos + margin)[:, None])
+    semi_min = neg.masked_fill(~semi, float("inf")).min(dim=1).values
+    hardest = torch.where(semi.any(dim=1), semi_min, neg.min(dim=1).values)
+    return F.relu(pos - hardest + margin).mean()
 
 
 # --------------------------------------------------------------------------
@@ -195,7 +282,7 @@ def retrieval_ranks_rows(f: torch.Tensor, c: torch.Tensor, row0: int = 0) -> tor
         gt = sim > d[:, None]
         gt[idx, row0 + idx] = False
         return gt.sum(dim=1).to(torch.int32) + 1
-    f32, c32 = _f32(f), _f32(c)
+    f32, c32 = _f32_pad4(f), _f32_pad4(c)
     L = N.lib()
     wsb = int(L.tt_rank_workspace_bytes(m))
     if wsb < 0:

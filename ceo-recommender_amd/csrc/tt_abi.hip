@@ -710,7 +710,7 @@ static bool nce_args_ok(const float* f, const float* c, int64_t m, int64_t n, in
 static std::once_flag g_nce_attr;
 static void nce_attrs() {
   std::call_once(g_nce_attr, [] {
-    const void* ks[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>,
+    const void* ks[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>, (const void*)k_nce_sim<2>,
                         (const void*)k_nce_dgrad<SRC_E_ROWS>, (const void*)k_nce_dgrad<SRC_E_AS_MK>};
     for (const void* k : ks)
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
@@ -880,6 +880,61 @@ int32_t tt_retrieval_ranks(const float* f, const float* c, int64_t m, int64_t n,
   hipLaunchKernelGGL(k_nce_sim<1>, dim3((unsigned)nblk), dim3(NTH), LDS_BYTES, s, g);
   hipLaunchKernelGGL(k_rank_finish, dim3((unsigned)std::min<int64_t>((m + 255) / 256, 4096)), dim3(256), 0, s, cnt,
                      m, ranks);
+  return launch_check();
+}
+
+// ---- semi_hard_negative_mining (contrastive.py:141-192) ----
+static int64_t triplet_ws_floats(int64_t m, int64_t n, int64_t* m_pad, int64_t* n_rp) {
+  using namespace tt::nce;
+  *m_pad = (m + 63) / 64 * 64;
+  *n_rp = ((n + BN - 1) / BN) * NWN;
+  return *m_pad + 2 * 2 * (*n_rp) * (*m_pad);  // diag | semi_part (u64) | all_part (u64)
+}
+
+int64_t tt_triplet_workspace_bytes(int64_t m, int64_t n, int32_t d) {
+  if (m < 1 || n < 1 || d < 4 || d % 4) return TT_ERR_ARG;
+  int64_t mp, nrp;
+  return triplet_ws_floats(m, n, &mp, &nrp) * (int64_t)sizeof(float);
+}
+
+int32_t tt_triplet_forward(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                           float margin, int64_t batch, void* ws, int64_t ws_bytes, int32_t* hardest,
+                           float* row_loss, float* loss, tt_stream_t stream) {
+  using namespace tt::nce;
+  if (!nce_args_ok(f, c, m, n, d, row0) || !ws || !hardest || !row_loss || !loss || batch < 2 || n < 2)
+    return TT_ERR_ARG;
+  int64_t mp, nrp;
+  if (triplet_ws_floats(m, n, &mp, &nrp) * (int64_t)sizeof(float) > ws_bytes) return TT_ERR_WORKSPACE;
+  nce_attrs();
+  hipStream_t s = (hipStream_t)stream;
+  float* diag = (float*)ws;
+  uint64_t* semi = (uint64_t*)((float*)ws + mp);
+  uint64_t* all = semi + nrp * mp;
+  hipLaunchKernelGGL(k_nce_diag, dim3((unsigned)(((m + 15) / 16 + 3) / 4)), dim3(256), 0, s, f, c, m, n, d, row0,
+                     1.0f, diag);
+  GemmArgs g = sim_args(f, c, m, n, d, row0);
+  g.diag = diag;
+  g.margin = margin;
+  g.semi_part = semi;
+  g.all_part = all;
+  g.m_pad = mp;
+  const int64_t nblk = ((m + BM - 1) / BM) * g.n_blocks_n;
+  hipLaunchKernelGGL(k_nce_sim<2>, dim3((unsigned)nblk), dim3(NTH), LDS_BYTES, s, g);
+  hipLaunchKernelGGL(k_triplet_finish, dim3((unsigned)std::min<int64_t>((m + 255) / 256, 4096)), dim3(256), 0, s,
+                     semi, all, nrp, mp, m, diag, margin, (float)(1.0 / (double)batch), hardest, row_loss, loss);
+  return launch_check();
+}
+
+int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                            int64_t batch, const int32_t* hardest, const float* row_loss, const float* grad_loss,
+                            float* df, float* dc, tt_stream_t stream) {
+  using namespace tt::nce;
+  if (!nce_args_ok(f, c, m, n, d, row0) || !hardest || !row_loss || !grad_loss || !df || !dc || batch < 2)
+    return TT_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  (void)hipMemsetAsync(dc, 0, sizeof(float) * n * d, s);
+  hipLaunchKernelGGL(k_triplet_bwd, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s, f, c, m, d, row0, hardest,
+                     row_loss, grad_loss, (float)(1.0 / (double)batch), df, dc);
   return launch_check();
 }
 

@@ -103,7 +103,38 @@ struct GemmArgs {
   // grad epilogue
   float* part;         // [split][M_tiles][N_tiles][256]
   int64_t p_nti, p_ntj;
+  // triplet (semi-hard mining) epilogue
+  float margin;
+  uint64_t* semi_part;  // [N / WN parts][M_pad] min key over semi-hard negatives
+  uint64_t* all_part;   // [N / WN parts][M_pad] min key over all negatives
 };
+
+// Orderable 64-bit key of a distance and its column: the float bits mapped
+// to an unsigned order (negative values flipped), column in the low word --
+// the minimum key is the smallest distance, ties to the lowest column.
+constexpr uint64_t KEY_NONE = ~0ull;
+__device__ __forceinline__ uint32_t ord_f32(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+// min over the 16 lanes (r) that share a row group g (DPP, no LDS)
+__device__ __forceinline__ uint64_t row_min16(uint64_t v) {
+  uint64_t o;
+  o = dpp_u64<0xB1>(v);  v = o < v ? o : v;   // quad_perm [1,0,3,2]
+  o = dpp_u64<0x4E>(v);  v = o < v ? o : v;   // quad_perm [2,3,0,1]
+  o = dpp_u64<0x141>(v); v = o < v ? o : v;   // row_half_mirror
+  o = dpp_u64<0x140>(v); v = o < v ? o : v;   // row_mirror
+  return v;
+}
 
 // ---- global -> registers (4 float4 per thread per operand per K chunk) ----
 template <int S>
@@ -320,6 +351,36 @@ __global__ __launch_bounds__(NTH) void k_nce_sim(GemmArgs a) {
       const int64_t gj = n0 + wn * WN + 16 * j + r;
       if (g == 0 && gj < a.n_pad) a.colpart[cpart * a.n_pad + gj] = v;
     }
+  } else if constexpr (MODE == 2) {
+    // semi-hard triplet mining (contrastive.py:163-190): dist = 1 - sim in
+    // fp32 as the reference rounds it; per row the smallest semi-hard
+    // negative (pos < dist < pos + margin) and the smallest negative overall
+    const int64_t rpart = bn * NWN + wn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t gi = m0 + wm * WM + 16 * i + 4 * g + q;
+        const float pos = 1.f - a.diag[gi < a.M ? gi : 0];
+        const float hi = pos + a.margin;
+        uint64_t ks = KEY_NONE, ka = KEY_NONE;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int64_t gj = n0 + wn * WN + 16 * j + r;
+          const float dist = 1.f - acc[i][j][q];
+          const bool ok = gj < a.N && gj != a.row0 + gi;
+          const uint64_t key = ((uint64_t)ord_f32(dist) << 32) | (uint32_t)gj;
+          ka = (ok && key < ka) ? key : ka;
+          ks = (ok && dist > pos && dist < hi && key < ks) ? key : ks;
+        }
+        ks = row_min16(ks);
+        ka = row_min16(ka);
+        if (r == 0 && gi < a.m_pad) {
+          a.semi_part[rpart * a.m_pad + gi] = ks;
+          a.all_part[rpart * a.m_pad + gi] = ka;
+        }
+      }
+    }
   } else {
     // rank: count j != row0 + i with sim_ij > sim_ii
 #pragma unroll
@@ -526,6 +587,61 @@ __global__ __launch_bounds__(256) void k_nce_loss(const float* __restrict__ rows
 __global__ __launch_bounds__(256) void k_rank_finish(const int* __restrict__ cnt, int64_t m, int* __restrict__ rank) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x)
     rank[e] = cnt[e] + 1;
+}
+
+// Per row: the hardest semi-hard negative if there is one, else the hardest
+// negative overall (contrastive.py:181-188); row_loss = relu(pos - hardest +
+// margin) (fp32, the reference's rounding), hardest[i] = its column;
+// loss += sum(row_loss) / batch.
+__global__ __launch_bounds__(256) void k_triplet_finish(const uint64_t* __restrict__ semi_part,
+                                                        const uint64_t* __restrict__ all_part, int64_t n_rp,
+                                                        int64_t m_pad, int64_t m, const float* __restrict__ diag,
+                                                        float margin, float inv_batch, int* __restrict__ hardest,
+                                                        float* __restrict__ row_loss, float* loss) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t ks = KEY_NONE, ka = KEY_NONE;
+    for (int64_t p = 0; p < n_rp; ++p) {
+      const uint64_t s = semi_part[p * m_pad + i], x = all_part[p * m_pad + i];
+      ks = s < ks ? s : ks;
+      ka = x < ka ? x : ka;
+    }
+    const uint64_t k = ks != KEY_NONE ? ks : ka;
+    const float hd = unord_f32((uint32_t)(k >> 32));
+    const float pos = 1.f - diag[i];
+    float li = (pos - hd) + margin;
+    li = li > 0.f ? li : 0.f;
+    hardest[i] = (int)(uint32_t)k;
+    row_loss[i] = li;
+    acc += li;
+  }
+  acc = wave_reduce(acc);
+  if (lane_id() == 0) red[wave_id()] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss, ((red[0] + red[1]) + (red[2] + red[3])) * inv_batch);
+}
+
+// Backward of the mined triplet loss: for every active row i (row_loss > 0)
+// with hardest column j, dL/dloss = g:  dF_i = (g / B) (c_j - c_{row0+i}),
+// dC_{row0+i} -= (g / B) f_i,  dC_j += (g / B) f_i.  One wave per row;
+// dF rows are owned, dC receives atomics (dc zeroed by the caller).
+__global__ __launch_bounds__(256) void k_triplet_bwd(const float* __restrict__ F, const float* __restrict__ C,
+                                                     int64_t m, int d, int64_t row0, const int* __restrict__ hardest,
+                                                     const float* __restrict__ row_loss, const float* __restrict__ g,
+                                                     float inv_batch, float* __restrict__ dF, float* __restrict__ dC) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + wave_id();
+  if (i >= m) return;
+  const float sc = row_loss[i] > 0.f ? *g * inv_batch : 0.f;
+  const int64_t j = hardest[i], ip = row0 + i;
+  for (int k = lane_id(); k < d; k += 64) {
+    const float fk = F[i * d + k];
+    dF[i * d + k] = sc * (C[j * d + k] - C[ip * d + k]);
+    if (sc != 0.f) {
+      atomicAdd(dC + ip * d + k, -sc * fk);
+      atomicAdd(dC + j * d + k, sc * fk);
+    }
+  }
 }
 
 }  // namespace nce

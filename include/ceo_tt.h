@@ -213,6 +213,26 @@ int32_t tt_retrieval_ranks(const float* f, const float* c, int64_t m, int64_t n,
                            int64_t row0, void* ws, int64_t ws_bytes, int32_t* ranks,
                            tt_stream_t stream);
 
+/* semi_hard_negative_mining (contrastive.py:141-192): dist = 1 - F C^T
+ * (fp32), pos_i = dist[i][row0+i]; per firm row i the hardest semi-hard
+ * negative (smallest dist with pos < dist < pos + margin over j != row0+i),
+ * else the hardest negative overall; row_loss[i] = relu(pos - hardest +
+ * margin), hardest[i] = its column (ties: lowest column),
+ * *loss += sum_i row_loss[i] / batch (caller zeroes it).  One fused
+ * similarity GEMM + masked-min epilogue replaces the reference's per-row
+ * Python loop.  Backward (autograd of the same expression): with
+ * g = *grad_loss, for each row with row_loss > 0:
+ *   df_i = (g/B)(c_j - c_{row0+i}),  dc_{row0+i} -= (g/B) f_i,  dc_j += (g/B) f_i;
+ * df [m, d] and dc [n, d] are overwritten.  ws: tt_triplet_workspace_bytes. */
+int64_t tt_triplet_workspace_bytes(int64_t m, int64_t n, int32_t d);
+int32_t tt_triplet_forward(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                           int64_t row0, float margin, int64_t batch, void* ws, int64_t ws_bytes,
+                           int32_t* hardest, float* row_loss, float* loss, tt_stream_t stream);
+int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                            int64_t row0, int64_t batch, const int32_t* hardest,
+                            const float* row_loss, const float* grad_loss, float* df, float* dc,
+                            tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

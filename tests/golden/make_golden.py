@@ -27,7 +27,10 @@ Fixtures:
       ``compute_retrieval_metrics`` (contrastive.py:52-72, 275-332) of a
       small ContrastiveCEOFirmMatcher (the embeddings are stored too).
 
-    python tests/golden/make_golden.py [contrastive]   # only that fixture
+  * ``triplet.npz``: ``semi_hard_negative_mining`` (contrastive.py:141-192)
+      loss + autograd dF/dC (fp32 and fp64) for B in {1, 2, 64, 96, 128, 256}.
+
+    python tests/golden/make_golden.py [contrastive|triplet]   # only that fixture
 """
 import contextlib
 import io
@@ -362,12 +365,51 @@ def gen_contrastive():
     print("wrote contrastive.npz:", {k: out[f"nce/{k}/loss"] for k in cases}, metrics)
 
 
+def gen_triplet():
+    """``semi_hard_negative_mining`` (contrastive.py:141-192): loss and
+    autograd dF/dC of the reference's per-row loop, fp32 and fp64, for
+    normalised / correlated / un-normalised pairs (B = 1 returns 0)."""
+    from ceo_firm_matching.contrastive import semi_hard_negative_mining
+    out = {}
+    g = torch.Generator().manual_seed(7)
+    nrm = torch.nn.functional.normalize
+    cases = {"b1": (1, 32, "norm"), "b2": (2, 32, "norm"), "b64": (64, 32, "norm"),
+             "b256": (256, 64, "norm"), "corr128": (128, 32, "corr"), "raw96": (96, 30, "raw")}
+    for name, (B, D, kind) in cases.items():
+        f = torch.randn(B, D, generator=g)
+        c = torch.randn(B, D, generator=g)
+        if kind == "norm":
+            f, c = nrm(f, dim=1), nrm(c, dim=1)
+        elif kind == "corr":  # positives close: a mix of semi-hard and fallback rows
+            f = nrm(f, dim=1)
+            c = nrm(f + 0.35 * c, dim=1)
+        else:
+            f, c = 0.3 * f, 0.3 * c
+        for tag, dt in (("", torch.float32), ("64", torch.float64)):
+            fx = f.to(dt).clone().requires_grad_(True)
+            cx = c.to(dt).clone().requires_grad_(True)
+            loss = semi_hard_negative_mining(fx, cx, margin=0.2)
+            out[f"tri/{name}/loss{tag}"] = np.float64(loss.item())
+            if loss.requires_grad:
+                loss.backward()
+                out[f"tri/{name}/df{tag}"] = fx.grad.numpy().astype(np.float32)
+                out[f"tri/{name}/dc{tag}"] = cx.grad.numpy().astype(np.float32)
+        out[f"tri/{name}/f"] = f.numpy().copy()
+        out[f"tri/{name}/c"] = c.numpy().copy()
+    np.savez_compressed(os.path.join(HERE, "triplet.npz"), **out)
+    print("wrote triplet.npz:", {k: out[f"tri/{k}/loss"] for k in cases})
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["contrastive"]:
         gen_contrastive()
+        sys.exit(0)
+    if sys.argv[1:] == ["triplet"]:
+        gen_triplet()
         sys.exit(0)
     for name, (meta, latent, B) in CASES.items():
         gen_case(name, meta, latent, B)
     gen_ddp()
     gen_cli()
     gen_contrastive()
+    gen_triplet()

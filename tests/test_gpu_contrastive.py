@@ -173,3 +173,97 @@ def test_info_nce_sharded_two_ranks():
         p.join(timeout=120)
     for rank, err in res:
         assert isinstance(err, float) and err < TOL, (rank, err)
+
+
+# ---------------------------------------------------------------------------
+# semi_hard_negative_mining (contrastive.py:141-192) on tt_triplet_*
+# ---------------------------------------------------------------------------
+AMBIG = 2e-6  # rows whose candidates sit this close to a selection boundary may
+              # legitimately select differently under another summation order
+
+
+def _triplet(f, c, margin=0.2):
+    from ceo_firm_matching.contrastive import semi_hard_mining
+    f = f.clone().requires_grad_(True)
+    c = c.clone().requires_grad_(True)
+    loss, hardest, row_loss = semi_hard_mining(f, c, margin)
+    loss.backward()
+    return loss.detach(), hardest, row_loss, f.grad, c.grad
+
+
+def _grads_given(f, c, j, act):
+    """closed-form grads (oracle algebra) for a given selection"""
+    B = f.shape[0]
+    w = act.double() / B
+    df = w[:, None] * (c[j] - c)
+    dc = -w[:, None] * f
+    dc.index_add_(0, j, w[:, None] * f)
+    return df, dc
+
+
+def _check_triplet(f, c, got, margin=0.2, ref_loss=None):
+    loss, hardest, row_loss, df, dc = got
+    f64, c64 = f.double(), c.double()
+    o = OC.semi_hard(f64, c64, margin)
+    ok = (o["slack"] > AMBIG)
+    hj = hardest.cpu().long()
+    rl = row_loss.cpu().double()
+    # unambiguous rows select exactly what the reference selects
+    assert torch.equal(hj[ok], o["hardest"][ok]), int((hj[ok] != o["hardest"][ok]).sum())
+    assert float((rl[ok] - o["row_loss"][ok]).abs().max()) <= 1e-5
+    assert int((~ok).sum()) <= max(2, f.shape[0] // 10)  # near-ties grow with B at small D
+    expect = torch.where(ok, o["row_loss"], rl).mean()
+    assert abs(float(loss) - float(expect)) <= TOL * max(1.0, float(expect))
+    if ref_loss is not None and bool(ok.all()):
+        assert abs(float(loss) - ref_loss) <= TOL * max(1.0, abs(ref_loss))
+    # backward kernel == the closed form for the selection it made
+    rdf, rdc = _grads_given(f64, c64, hj, rl > 0)
+    assert normwise(df.cpu().numpy(), rdf.numpy()) < TOL
+    assert normwise(dc.cpu().numpy(), rdc.numpy()) < TOL
+
+
+@pytest.mark.parametrize("case", ["b2", "b64", "b256", "corr128", "raw96"])
+def test_semi_hard_golden(case):
+    dev = _dev()
+    g = load_golden("triplet")
+    f = torch.from_numpy(g[f"tri/{case}/f"])
+    c = torch.from_numpy(g[f"tri/{case}/c"])
+    got = _triplet(f.to(dev), c.to(dev))
+    _check_triplet(f, c, got, ref_loss=float(g[f"tri/{case}/loss64"]))
+    o = OC.semi_hard(f.double(), c.double())
+    if bool((o["slack"] > AMBIG).all()):  # then the reference's own autograd grads too
+        assert normwise(got[3].cpu().numpy(), g[f"tri/{case}/df64"]) < TOL
+        assert normwise(got[4].cpu().numpy(), g[f"tri/{case}/dc64"]) < TOL
+
+
+def test_semi_hard_b1_is_zero():
+    from ceo_firm_matching.contrastive import semi_hard_negative_mining
+    dev = _dev()
+    x = torch.randn(1, 32, device=dev)
+    assert float(semi_hard_negative_mining(x, x)) == 0.0
+
+
+@pytest.mark.parametrize("B,D,mix", [(1000, 64, 0.5), (4100, 32, 0.5), (517, 36, 0.5), (2048, 30, 0.5),
+                                     (3000, 256, 0.0), (700, 128, 2.0)])
+def test_semi_hard_ragged_vs_oracle(B, D, mix):
+    """Partial tiles, several column blocks, D not a multiple of 4 (padded),
+    both selection branches."""
+    dev = _dev()
+    gen = torch.Generator().manual_seed(B + D)
+    f = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(B, D, generator=gen) + mix * f, dim=1)
+    got = _triplet(f.to(dev), c.to(dev))
+    _check_triplet(f, c, got)
+
+
+def test_semi_hard_matches_aten_reference_expression():
+    """semi_hard_negative_mining on a HIP tensor == the package's ATen
+    expression of the reference loop on CPU (same inputs)."""
+    from ceo_firm_matching.contrastive import semi_hard_negative_mining
+    dev = _dev()
+    gen = torch.Generator().manual_seed(9)
+    f = torch.nn.functional.normalize(torch.randn(300, 48, generator=gen), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(300, 48, generator=gen) + 0.4 * f, dim=1)
+    a = semi_hard_negative_mining(f.to(dev), c.to(dev))
+    b = semi_hard_negative_mining(f, c)
+    assert abs(float(a) - float(b)) <= TOL * max(1.0, float(b))

@@ -10,6 +10,7 @@ from .engine import FusedTrainer
 from .model import CEOFirmMatcher
 from .synthetic import generate_pairs, generate_synthetic_data
 from .training import train, train_model
+from . import contrastive  # noqa: E402  (reference: Extension 2, contrastive learning)
 
 __version__ = "0.4.0+mi355x"
 

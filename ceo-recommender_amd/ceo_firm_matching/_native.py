@@ -90,6 +90,8 @@ def lib() -> ctypes.CDLL:
         "tt_workspace_bytes": (I64, [D, I64]),
         "tt_forward": (I32, [D, P, P, P, Bt, I32, U64, I64, P, I64, P, P]),
         "tt_backward": (I32, [D, P, Bt, P, U64, I64, P, I64, P, P]),
+        "tt_embed_forward": (I32, [D, P, P, P, Bt, I32, U64, I64, P, I64, P, P]),
+        "tt_embed_backward": (I32, [D, P, Bt, P, U64, I64, P, I64, P, P]),
         "tt_train_step": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P]),
         "tt_train_step_ev": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P, ctypes.POINTER(P)]),
         "tt_adam_apply": (I32, [P, P, P, P, I64, H, P, I64, P]),

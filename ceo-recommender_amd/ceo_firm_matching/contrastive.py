@@ -12,9 +12,14 @@ SURVEY 8a rows a18/a19, BASELINE cfg 5:
   all-reduce of the column sums and of the loss, reduce-scatter of dC.
 * ``retrieval_ranks`` / ``compute_retrieval_metrics`` (contrastive.py:275-332):
   rank of the true match among all candidates, recall@1/5/k, MRR, median rank.
+* ``semi_hard_negative_mining`` (contrastive.py:141-192): triplet loss with
+  semi-hard negatives as one fused similarity GEMM + masked-min kernel
+  (tt_triplet_*) instead of a per-row Python loop.
 * ``ContrastiveCEOFirmMatcher`` (contrastive.py:21-99): the reference's module
-  tree (base CEOFirmMatcher + projector heads) so ``get_embeddings`` callers
-  work unchanged.
+  tree (base CEOFirmMatcher + projector heads); on a HIP device the towers
+  run in the fused kernels (tt_embed_forward / tt_embed_backward).
+* ``train_contrastive`` (contrastive.py:197-272): combined regression +
+  contrastive training loop with the reference's printed lines.
 
 On CPU tensors every function evaluates the reference's ATen expression.
 """
@@ -28,6 +33,8 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
+import torch.optim as optim
+from torch.utils.data import DataLoader
 
 from . import _native as N
 from .config import Config
@@ -337,14 +344,61 @@ class ContrastiveCEOFirmMatcher(nn.Module):
         self.ceo_projector = nn.Sequential(nn.Linear(D, D), nn.ReLU(), nn.Linear(D, D // 2))
 
     def get_embeddings(self, f_numeric, f_cat, c_numeric, c_cat):
-        b = self.base_model
-        f_embs = [emb(f_cat[:, i]) for i, emb in enumerate(b.firm_embeddings)]
-        u = b.firm_tower(torch.cat([f_numeric] + f_embs, dim=1))
-        c_embs = [emb(c_cat[:, i]) for i, emb in enumerate(b.ceo_embeddings)]
-        v = b.ceo_tower(torch.cat([c_numeric] + c_embs, dim=1))
+        """L2-normalised tower outputs (contrastive.py:52-72); the towers run
+        in the fused HIP kernels on a HIP device (tt_embed_forward)."""
+        u, v = self.base_model.tower_embeddings(f_numeric, f_cat, c_numeric, c_cat)
         return F.normalize(u, dim=1), F.normalize(v, dim=1)
 
     def forward(self, f_numeric, f_cat, c_numeric, c_cat):
         u, v = self.get_embeddings(f_numeric, f_cat, c_numeric, c_cat)
         match_score = (u * v).sum(dim=1, keepdim=True) * self.base_model.logit_scale.exp()
         return match_score, F.normalize(self.firm_projector(u), dim=1), F.normalize(self.ceo_projector(v), dim=1)
+
+
+# --------------------------------------------------------------------------
+# combined regression + contrastive training (contrastive.py:197-272)
+# --------------------------------------------------------------------------
+def train_contrastive(train_loader: DataLoader, val_loader: DataLoader, metadata: Dict[str, int], config: Config,
+                      contrastive_weight: float = 0.3, temperature: float = 0.07,
+                      use_triplet: bool = False) -> ContrastiveCEOFirmMatcher:
+    """Train the two-tower model on (1 - a) * weighted MSE + a * InfoNCE (or
+    semi-hard triplet) loss -- reference contrastive.py:197-272, same
+    signature, same prints, same batch order (the loader is iterated as is).
+
+    On a HIP device the towers run forward and backward in the fused kernels
+    (one autograd node for both encoders), InfoNCE / triplet mining in the
+    similarity kernels; the projector heads, the match score and Adam are
+    ATen ops.  Loss totals stay on the device until an epoch is printed
+    (the reference syncs three times per step with ``.item()``)."""
+    model = ContrastiveCEOFirmMatcher(metadata, config).to(config.DEVICE)
+    optimizer = optim.Adam(model.parameters(), lr=config.LEARNING_RATE)
+
+    print(f"Training Contrastive Two-Tower on {config.DEVICE}")
+    print(f"  Contrastive weight: {contrastive_weight}")
+    print(f"  Temperature: {temperature}")
+    print(f"  Loss type: {'Triplet' if use_triplet else 'InfoNCE'}")
+
+    dev = torch.device(config.DEVICE)
+    for epoch in range(config.EPOCHS):
+        model.train()
+        totals = torch.zeros(3, dtype=torch.float64, device=dev)  # loss, mse, cl
+        n_batches = 0
+        for batch in train_loader:
+            batch = {k: v.to(dev) for k, v in batch.items()}
+            optimizer.zero_grad()
+            match_score, firm_proj, ceo_proj = model(batch['firm_numeric'], batch['firm_cat'],
+                                                     batch['ceo_numeric'], batch['ceo_cat'])
+            mse_loss = (batch['weights'] * (match_score - batch['target']) ** 2).mean()
+            if use_triplet:
+                cl_loss = semi_hard_negative_mining(firm_proj, ceo_proj)
+            else:
+                cl_loss = info_nce_loss(firm_proj, ceo_proj, temperature)
+            loss = (1 - contrastive_weight) * mse_loss + contrastive_weight * cl_loss
+            loss.backward()
+            optimizer.step()
+            totals += torch.stack([loss.detach(), mse_loss.detach(), cl_loss.detach().to(mse_loss.dtype)]).double()
+            n_batches += 1
+        if epoch % 5 == 0:
+            avg_loss, avg_mse, avg_cl = (totals / max(n_batches, 1)).tolist()
+            print(f"  Epoch {epoch}: Loss={avg_loss:.4f} (MSE={avg_mse:.4f}, CL={avg_cl:.4f})")
+    return model

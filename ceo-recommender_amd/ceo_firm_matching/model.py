@@ -164,6 +164,16 @@ class CEOFirmMatcher(nn.Module):
             return _fused_forward(self, f_numeric, f_cat, c_numeric, c_cat)
         return self._aten_forward(f_numeric, f_cat, c_numeric, c_cat)
 
+    def tower_embeddings(self, f_numeric, f_cat, c_numeric, c_cat):
+        """(U, V): the raw firm / CEO tower outputs (model.py:69-77, before the
+        L2 normalisation) -- the encoder half that contrastive.py:52-72
+        get_embeddings builds on.  One fused autograd node on a HIP device."""
+        if f_numeric.device.type == "cuda":
+            return _fused_embeddings(self, f_numeric, f_cat, c_numeric, c_cat)
+        f = torch.cat([f_numeric] + [e(f_cat[:, i]) for i, e in enumerate(self.firm_embeddings)], dim=1)
+        c = torch.cat([c_numeric] + [e(c_cat[:, i]) for i, e in enumerate(self.ceo_embeddings)], dim=1)
+        return self.firm_tower(f), self.ceo_tower(c)
+
     def _aten_forward(self, f_numeric, f_cat, c_numeric, c_cat):
         """CPU evaluation of model.py:67-89 with ATen ops (no HIP device)."""
         if not self._aten_warned:
@@ -241,10 +251,61 @@ class _FusedTwoTower(torch.autograd.Function):
         return (None, None, None, None, None, *grads)
 
 
+class _FusedTowerEmbeddings(torch.autograd.Function):
+    """Raw tower outputs (U, V) of both towers as one autograd node
+    (tt_embed_forward / tt_embed_backward): the encoder half of the model for
+    callers that score embeddings themselves (contrastive.py:52-99)."""
+
+    @staticmethod
+    def forward(ctx, model, f_num, f_cat, c_num, c_cat, *params):
+        arena = model._arena
+        B = f_num.shape[0]
+        D = arena.desc.latent
+        train = bool(model.training)
+        ws_bytes = N.workspace_bytes(arena.desc, max(B, 1))
+        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=f_num.device)
+        emb = torch.empty(2, B, D, dtype=torch.float32, device=f_num.device)
+        seed, step = model.next_dropout_stream() if train else (0, 0)
+        batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
+        rc = N.lib().tt_embed_forward(arena.desc, arena.params.data_ptr(), arena.buffers.data_ptr(),
+                                      arena.nbt.data_ptr(), batch, int(train), seed, step, ws.data_ptr(), ws_bytes,
+                                      emb.data_ptr(), N.stream_ptr(f_num.device))
+        N.check(rc, "tt_embed_forward", B, 64)
+        ctx.model, ctx.train, ctx.seed, ctx.step = model, train, seed, step
+        ctx.ws, ctx.ws_bytes = ws, ws_bytes
+        ctx.save_for_backward(f_num, f_cat, c_num, c_cat)
+        return emb[0], emb[1]
+
+    @staticmethod
+    def backward(ctx, du, dv):
+        if not ctx.train:
+            raise NotImplementedError("backward through eval-mode tower embeddings is not supported by the "
+                                      "fused kernels (call model.train())")
+        f_num, f_cat, c_num, c_cat = ctx.saved_tensors
+        model = ctx.model
+        arena = model._arena
+        B = f_num.shape[0]
+        D = arena.desc.latent
+        demb = torch.zeros(2, B, D, dtype=torch.float32, device=f_num.device)
+        if du is not None:
+            demb[0].copy_(du)
+        if dv is not None:
+            demb[1].copy_(dv)
+        grad = torch.empty_like(arena.params)
+        batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
+        rc = N.lib().tt_embed_backward(arena.desc, arena.params.data_ptr(), batch, demb.data_ptr(), ctx.seed,
+                                       ctx.step, ctx.ws.data_ptr(), ctx.ws_bytes, grad.data_ptr(),
+                                       N.stream_ptr(f_num.device))
+        N.check(rc, "tt_embed_backward", B, 64)
+        offs = N.param_offsets(arena.desc)
+        grads = [grad[off:off + p.numel()].view_as(p) for _, p, off in model._named_slots(offs)]
+        return (None, None, None, None, None, *grads)
+
+
 _POISON_WS = bool(os.environ.get("CEO_TT_POISON_WS"))
 
 
-def _fused_forward(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
+def _fused_inputs(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
     dev = f_numeric.device
     if model.logit_scale.device != dev:
         raise RuntimeError(f"CEOFirmMatcher parameters are on {model.logit_scale.device}, inputs on {dev}")
@@ -262,4 +323,14 @@ def _fused_forward(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
     if f_num.shape[0] != c_num.shape[0]:
         raise RuntimeError("firm and CEO batches differ in size")
     params = [p for _, p, _ in model._named_slots(N.param_offsets(model._arena.desc))]
+    return f_num, f_cat, c_num, c_cat, params
+
+
+def _fused_forward(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
+    f_num, f_cat, c_num, c_cat, params = _fused_inputs(model, f_numeric, f_cat, c_numeric, c_cat)
     return _FusedTwoTower.apply(model, f_num, f_cat, c_num, c_cat, *params)
+
+
+def _fused_embeddings(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
+    f_num, f_cat, c_num, c_cat, params = _fused_inputs(model, f_numeric, f_cat, c_numeric, c_cat)
+    return _FusedTowerEmbeddings.apply(model, f_num, f_cat, c_num, c_cat, *params)

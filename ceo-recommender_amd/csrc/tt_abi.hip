@@ -149,8 +149,10 @@ static void set_lds_attrs() {
                         (const void*)k_l0_fwd<ROWS, 4, true>, (const void*)k_l0_fwd<ROWS, 4, false>,
                         (const void*)k_l0_fwd<ROWS, 8, true>, (const void*)k_l0_fwd<ROWS, 8, false>,
                         (const void*)k_l4_fwd<ROWS>,
-                        (const void*)k_top<4, 64>,        (const void*)k_top<8, 64>,
-                        (const void*)k_top<4, 128>,       (const void*)k_top<8, 128>,
+                        (const void*)k_top<4, 64, false>, (const void*)k_top<8, 64, false>,
+                        (const void*)k_top<4, 128, false>, (const void*)k_top<8, 128, false>,
+                        (const void*)k_top<4, 64, true>,  (const void*)k_top<8, 64, true>,
+                        (const void*)k_top<4, 128, true>, (const void*)k_top<8, 128, true>,
                         (const void*)k_bwd_mid<ROWS>,    (const void*)k_bwd_first<ROWS>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   });
@@ -399,16 +401,23 @@ static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev =
 static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
   launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
-static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev = {}) {
+template <bool EMB>
+static void launch_top_t(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev) {
   const dim3 grid(P.n_tiles_top, grid_y), blk(4 * P.top_rows);
   if (P.ndt == 4 && P.top_rows == 64)
-    launch(k_top<4, 64>, grid, blk, P.lds_top, s, ev, a);
+    launch(k_top<4, 64, EMB>, grid, blk, P.lds_top, s, ev, a);
   else if (P.ndt == 4)
-    launch(k_top<4, 128>, grid, blk, P.lds_top, s, ev, a);
+    launch(k_top<4, 128, EMB>, grid, blk, P.lds_top, s, ev, a);
   else if (P.top_rows == 64)
-    launch(k_top<8, 64>, grid, blk, P.lds_top, s, ev, a);
+    launch(k_top<8, 64, EMB>, grid, blk, P.lds_top, s, ev, a);
   else
-    launch(k_top<8, 128>, grid, blk, P.lds_top, s, ev, a);
+    launch(k_top<8, 128, EMB>, grid, blk, P.lds_top, s, ev, a);
+}
+static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev = {}) {
+  if (a.mode == TOP_EMB_FWD || a.mode == TOP_EMB_BWD)
+    launch_top_t<true>(a, P, grid_y, s, ev);
+  else
+    launch_top_t<false>(a, P, grid_y, s, ev);
 }
 
 }  // namespace tt
@@ -446,10 +455,10 @@ int64_t tt_workspace_bytes(const tt_model_desc* d, int64_t max_batch) {
   return make_ws(L, max_batch).total * (int64_t)sizeof(float);
 }
 
-int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, int64_t* nbt, const tt_batch* b,
-                   int32_t train, uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* score,
-                   tt_stream_t stream) {
-  if (!params || !buffers || !nbt || !ws || !score) return TT_ERR_ARG;
+static int32_t forward_impl(const tt_model_desc* d, const float* params, float* buffers, int64_t* nbt,
+                            const tt_batch* b, int32_t train, uint64_t seed, int64_t step, void* ws,
+                            int64_t ws_bytes, float* score, float* emb, tt_stream_t stream) {
+  if (!params || !buffers || !nbt || !ws || (!score && !emb)) return TT_ERR_ARG;
   Ctx c;
   int rc = prepare(d, b, ws_bytes, train ? 2 : 0, &c);
   if (rc) return rc;
@@ -462,8 +471,9 @@ int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, 
   a.update_stats = a.train;
   a.seed = seed;
   a.step_host = step;
-  a.mode = TOP_FWD;
+  a.mode = emb ? TOP_EMB_FWD : TOP_FWD;
   a.score = score;
+  a.emb = emb;
   if (train) {
     for (int t = 0; t < 2; ++t) {
       (void)hipMemsetAsync(w + c.W.st0[t], 0, sizeof(float) * NREP * 2 * H0, s);
@@ -476,9 +486,24 @@ int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, 
   return launch_check();
 }
 
-int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch* b, const float* dscore,
-                    uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream) {
-  if (!params || !dscore || !ws || !grad) return TT_ERR_ARG;
+int32_t tt_forward(const tt_model_desc* d, const float* params, float* buffers, int64_t* nbt, const tt_batch* b,
+                   int32_t train, uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* score,
+                   tt_stream_t stream) {
+  if (!score) return TT_ERR_ARG;
+  return forward_impl(d, params, buffers, nbt, b, train, seed, step, ws, ws_bytes, score, nullptr, stream);
+}
+
+int32_t tt_embed_forward(const tt_model_desc* d, const float* params, float* buffers, int64_t* nbt,
+                         const tt_batch* b, int32_t train, uint64_t seed, int64_t step, void* ws, int64_t ws_bytes,
+                         float* emb, tt_stream_t stream) {
+  if (!emb) return TT_ERR_ARG;
+  return forward_impl(d, params, buffers, nbt, b, train, seed, step, ws, ws_bytes, nullptr, emb, stream);
+}
+
+static int32_t backward_impl(const tt_model_desc* d, const float* params, const tt_batch* b, const float* dscore,
+                             const float* demb, uint64_t seed, int64_t step, void* ws, int64_t ws_bytes,
+                             float* grad, tt_stream_t stream) {
+  if (!params || (!dscore && !demb) || !ws || !grad) return TT_ERR_ARG;
   Ctx c;
   int rc = prepare(d, b, ws_bytes, 2, &c);
   if (rc) return rc;
@@ -491,8 +516,9 @@ int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch*
   a.update_stats = 0;
   a.seed = seed;
   a.step_host = step;
-  a.mode = TOP_BWD_GIVEN;
+  a.mode = demb ? TOP_EMB_BWD : TOP_BWD_GIVEN;
   a.dscore = dscore;
+  a.demb = demb;
   (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
   for (int t = 0; t < 2; ++t) (void)hipMemsetAsync(w + c.W.bng[t], 0, sizeof(float) * NREP * BNG, s);
   (void)hipMemsetAsync(w + c.W.lsr, 0, sizeof(float) * NREP * LSR, s);
@@ -503,6 +529,18 @@ int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch*
   const int nb = (int)((c.L.n + RED_E - 1) / RED_E);
   hipLaunchKernelGGL(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, r);
   return launch_check();
+}
+
+int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch* b, const float* dscore,
+                    uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream) {
+  if (!dscore) return TT_ERR_ARG;
+  return backward_impl(d, params, b, dscore, nullptr, seed, step, ws, ws_bytes, grad, stream);
+}
+
+int32_t tt_embed_backward(const tt_model_desc* d, const float* params, const tt_batch* b, const float* demb,
+                          uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream) {
+  if (!demb) return TT_ERR_ARG;
+  return backward_impl(d, params, b, nullptr, demb, seed, step, ws, ws_bytes, grad, stream);
 }
 
 static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,

@@ -297,7 +297,7 @@ struct TowerDev {
   int64_t so_W0, so_b0, so_W4, so_b4, so_W8, so_b8;  // offsets inside one slab
 };
 
-enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2 };
+enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2, TOP_EMB_FWD = 3, TOP_EMB_BWD = 4 };
 
 struct StepArgs {
   TowerDev tw[2];
@@ -323,6 +323,8 @@ struct StepArgs {
   float* score;          // [B] output scores (nullable)
   const float* dscore;   // [B] upstream grad (TOP_BWD_GIVEN)
   float* tgw;            // [Bpad][2] (target, weight) of each batch row, gathered by k_l0_fwd
+  float* emb;            // [2][B][D] raw tower outputs U | V (TOP_EMB_FWD)
+  const float* demb;     // [2][B][D] upstream dU | dV (TOP_EMB_BWD)
 };
 
 // ---------------------------------------------------------------------------

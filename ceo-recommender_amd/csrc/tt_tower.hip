@@ -636,7 +636,11 @@ __device__ __forceinline__ int swz_a(int rr) {
 __device__ __forceinline__ int swz_w(int d) { return ((d >> 2) & 1) << 2; }
 
 
-template <int NDT, int R>
+// EMB instances serve the tower-embedding entry points (tt_embed_*):
+// TOP_EMB_FWD stores the raw tower outputs U, V (model.py:76-77 before the
+// normalisation) and stops; TOP_EMB_BWD takes dU / dV from the caller
+// instead of the cosine/MSE closed form.  Everything from dU on is shared.
+template <int NDT, int R, bool EMB>
 __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   using L = TopLds<NDT, R>;
   constexpr int NTH = R * 4, NW = R / 16, DP = L::DP;
@@ -645,7 +649,7 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   static_assert(NDT % 2 == 0, "a dA1 K step pairs two latent tiles");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
-  const bool bwd = a.mode != TOP_FWD;
+  const bool bwd = a.mode != TOP_FWD && a.mode != TOP_EMB_FWD;
   const int own = bwd ? (int)blockIdx.y : 0;
   const int oth = 1 - own;
   const int64_t step = step_current(a);
@@ -687,6 +691,16 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     wt = v.y;
   } else if (a.mode == TOP_BWD_GIVEN) {
     tg = a.dscore[min(row, a.B - 1)];
+  }
+  f32x4 dem[EMB ? NDT : 1];  // TOP_EMB_BWD: this lane's dU slice (issued with the other loads)
+  if constexpr (EMB) {
+    if (bwd) {
+      const float* src = a.demb + ((int64_t)own * a.B + min(row, a.B - 1)) * D;
+#pragma unroll
+      for (int j = 0; j < NDT; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dem[j][i] = src[min(16 * j + 4 * g + i, D - 1)];
+    }
   }
   RepSum2<NTH, 2 * H1> rs;
   if (a.train) rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
@@ -776,20 +790,42 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
       }
     };
     bf16x8 fo[2][3], fs[2][3];
-    ld(0, fo[0], fs[0]);
+    if (!(EMB && bwd)) {  // the embedding backward needs no forward recompute
+      ld(0, fo[0], fs[0]);
 #pragma unroll
-    for (int j = 0; j < NDT; ++j) {
-      if (j + 1 < NDT) ld(j + 1, fo[(j + 1) & 1], fs[(j + 1) & 1]);
-      accO[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + 16 * j + 4 * g);  // bias first: U = b + sum
-      accS[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + DP + 16 * j + 4 * g);
-      mfma_x3(fo[j & 1], po, accO[j]);
-      mfma_x3(fs[j & 1], ps, accS[j]);
+      for (int j = 0; j < NDT; ++j) {
+        if (j + 1 < NDT) ld(j + 1, fo[(j + 1) & 1], fs[(j + 1) & 1]);
+        accO[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + 16 * j + 4 * g);  // bias first: U = b + sum
+        accS[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + DP + 16 * j + 4 * g);
+        mfma_x3(fo[j & 1], po, accO[j]);
+        mfma_x3(fs[j & 1], ps, accS[j]);
+      }
+    }
+  }
+  const bool valid = row < a.B;
+  if constexpr (EMB) {
+    if (!bwd) {  // TOP_EMB_FWD (own = firm): U -> emb[0][row], V -> emb[1][row]
+      if (valid) {
+#pragma unroll
+        for (int j = 0; j < NDT; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int d = 16 * j + 4 * g + i;
+            if (d < D) {
+              a.emb[row * D + d] = accS[j][i];
+              a.emb[(a.B + row) * D + d] = accO[j][i];
+            }
+          }
+      }
+      return;
     }
   }
   if (bwd) __syncthreads();  // W8oth (dU region) read by every wave; A1 image complete
   TT_STAMP(2, 3);
 
   // ---- cosine, one row per lane
+  float ka = 0.f, kb = 0.f;
+  if constexpr (!EMB) {
   const float s = expf(lsc);
   float uv = 0.f, oo = 0.f, tt2 = 0.f;
 #pragma unroll
@@ -807,7 +843,6 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   const float int_ = __builtin_amdgcn_rsqf(tt2);
   const float cs = uv * ino * int_;
   const float sc = cs * s;
-  const bool valid = row < a.B;
   float ds = 0.f, loss_p = 0.f;
   if (a.mode == TOP_TRAIN) {
     const float diff = sc - tg;
@@ -833,8 +868,9 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
   // split into planes per K step t (latent tiles 2t, 2t+1): stored into the
   // dU image for dW8 and used at once as the B operand of dA1^T
   const float dc = ds * s;
-  const float ka = valid ? dc * ino * int_ : 0.f;
-  const float kb = valid ? dc * cs * ino * ino : 0.f;
+  ka = valid ? dc * ino * int_ : 0.f;
+  kb = valid ? dc * cs * ino * ino : 0.f;
+  }  // !EMB
   const int qd = (l & 15) >> 2, pc = l & 3;  // transposed read: row q, chunk p of this lane
   const int su = swz_u<L::CH>(rl);
   uint16_t* dUs = hs + L::dUi;
@@ -842,10 +878,19 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
 #pragma unroll
   for (int t = 0; t < NDT / 2; ++t) {
     float x[8];
+    if constexpr (EMB) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      x[i] = ka * accO[2 * t][i] - kb * accS[2 * t][i];
-      x[4 + i] = ka * accO[2 * t + 1][i] - kb * accS[2 * t + 1][i];
+      for (int i = 0; i < 4; ++i) {
+        const int d0 = 32 * t + 4 * g + i;
+        x[i] = (valid && d0 < D) ? dem[2 * t][i] : 0.f;
+        x[4 + i] = (valid && d0 + 16 < D) ? dem[2 * t + 1][i] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[i] = ka * accO[2 * t][i] - kb * accS[2 * t][i];
+        x[4 + i] = ka * accO[2 * t + 1][i] - kb * accS[2 * t + 1][i];
+      }
     }
     bf16x8 du[3];
     split8x3(x, du);
@@ -1318,10 +1363,14 @@ TT_L0(4)
 TT_L0(8)
 #undef TT_L0
 template __global__ void k_l4_fwd<64>(StepArgs);
-template __global__ void k_top<4, 64>(StepArgs);
-template __global__ void k_top<8, 64>(StepArgs);
-template __global__ void k_top<4, 128>(StepArgs);
-template __global__ void k_top<8, 128>(StepArgs);
+template __global__ void k_top<4, 64, false>(StepArgs);
+template __global__ void k_top<8, 64, false>(StepArgs);
+template __global__ void k_top<4, 128, false>(StepArgs);
+template __global__ void k_top<8, 128, false>(StepArgs);
+template __global__ void k_top<4, 64, true>(StepArgs);
+template __global__ void k_top<8, 64, true>(StepArgs);
+template __global__ void k_top<4, 128, true>(StepArgs);
+template __global__ void k_top<8, 128, true>(StepArgs);
 template __global__ void k_bwd_mid<64>(StepArgs);
 template __global__ void k_bwd_first<64>(StepArgs);
 

@@ -129,6 +129,19 @@ int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch*
                     const float* dscore, uint64_t seed, int64_t step,
                     void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream);
 
+/* Tower embeddings: the raw tower outputs U = firm_tower(x_f), V =
+ * ceo_tower(x_c) before the L2 normalisation (contrastive.py:52-72
+ * get_embeddings; model.py:69-77).  emb is [2][B][latent]: U rows then V
+ * rows.  Same BatchNorm / dropout semantics and workspace contract as
+ * tt_forward; tt_embed_backward takes demb = dL/d(emb) [2][B][latent] and
+ * writes the full flat gradient (logit_scale's entry is 0).               */
+int32_t tt_embed_forward(const tt_model_desc* d, const float* params, float* buffers, int64_t* nbt,
+                         const tt_batch* b, int32_t train, uint64_t seed, int64_t step,
+                         void* ws, int64_t ws_bytes, float* emb, tt_stream_t stream);
+int32_t tt_embed_backward(const tt_model_desc* d, const float* params, const tt_batch* b,
+                          const float* demb, uint64_t seed, int64_t step,
+                          void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream);
+
 /* One fused training step = training.py:44-57: forward, weighted MSE,
  * backward, and (apply_adam=1) the Adam update.  With apply_adam=0 only grad
  * is produced (data-parallel: all-reduce grad, then tt_adam_apply).

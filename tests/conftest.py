@@ -48,6 +48,8 @@ def normwise(a, b):
 # fp32 gives ~1e-6 noise and Adam turns noise into +-lr updates -> not
 # comparable across implementations.
 def excluded_param(name):
+    if name.startswith("base_model."):  # ContrastiveCEOFirmMatcher wraps the base model
+        name = name[len("base_model."):]
     return any(name.startswith(f"{t}_tower.{i}.bias") for t in ("firm", "ceo") for i in ("0", "4"))
 
 

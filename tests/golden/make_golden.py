@@ -30,7 +30,10 @@ Fixtures:
   * ``triplet.npz``: ``semi_hard_negative_mining`` (contrastive.py:141-192)
       loss + autograd dF/dC (fp32 and fp64) for B in {1, 2, 64, 96, 128, 256}.
 
-    python tests/golden/make_golden.py [contrastive|triplet]   # only that fixture
+  * ``contrastive_train.npz``: ``train_contrastive`` (contrastive.py:197-272),
+      InfoNCE and triplet: one-step grads and a 2-epoch run (prints, final state).
+
+    python tests/golden/make_golden.py [contrastive|triplet|contrastive_train]   # only that fixture
 """
 import contextlib
 import io
@@ -400,7 +403,73 @@ def gen_triplet():
     print("wrote triplet.npz:", {k: out[f"tri/{k}/loss"] for k in cases})
 
 
+def gen_contrastive_train():
+    """``train_contrastive`` (contrastive.py:197-272) on the CLI fixture's
+    train split (cli.npz), default Config (LATENT 60 -> 30-wide projections),
+    dropout disabled, batch 128 (6 full + 1 partial batch), InfoNCE and
+    triplet: (a) one step from the seeded init -- losses and every
+    parameter's grad; (b) EPOCHS=2 of the real loop -- printed lines and the
+    final state_dict."""
+    from torch.utils.data import DataLoader
+    from ceo_firm_matching.contrastive import (ContrastiveCEOFirmMatcher, info_nce_loss,
+                                               semi_hard_negative_mining, train_contrastive)
+    from ceo_firm_matching.data import CEOFirmDataset
+    cli = np.load(os.path.join(HERE, "cli.npz"), allow_pickle=False)
+    data = {k: torch.from_numpy(cli[f"train/{k}"]) for k in
+            ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")}
+    meta = {"n_firm_numeric": int(cli["meta/n_firm_numeric"]), "firm_cat_counts": list(cli["meta/firm_cat_counts"]),
+            "n_ceo_numeric": int(cli["meta/n_ceo_numeric"]), "ceo_cat_counts": list(cli["meta/ceo_cat_counts"])}
+    data.update(meta)
+    orig_dropout = torch.nn.Dropout.__init__
+
+    def no_dropout(self, p=0.5, inplace=False):
+        orig_dropout(self, 0.0, inplace)
+
+    out = {}
+    torch.nn.Dropout.__init__ = no_dropout
+    try:
+        for trip in (False, True):
+            tag = "tri" if trip else "nce"
+            cfg = ref.Config()
+            cfg.EPOCHS = 2
+            cfg.DEVICE = torch.device("cpu")
+            # (a) one step
+            torch.manual_seed(77)
+            m = ContrastiveCEOFirmMatcher(meta, cfg)
+            put(out, f"{tag}/init", m.state_dict())
+            m.train()
+            b = {k: data[k][:128] for k in ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")}
+            ms, fp, cp = m(b["firm_numeric"], b["firm_cat"], b["ceo_numeric"], b["ceo_cat"])
+            mse = (b["weights"] * (ms - b["target"]) ** 2).mean()
+            cl = semi_hard_negative_mining(fp, cp) if trip else info_nce_loss(fp, cp, 0.07)
+            loss = 0.7 * mse + 0.3 * cl
+            loss.backward()
+            out[f"{tag}/step/mse"] = np.float64(mse.item())
+            out[f"{tag}/step/cl"] = np.float64(cl.item())
+            out[f"{tag}/step/loss"] = np.float64(loss.item())
+            out[f"{tag}/step/match_score"] = ms.detach().numpy().copy()
+            out[f"{tag}/step/firm_proj"] = fp.detach().numpy().copy()
+            put(out, f"{tag}/grad", {n: p.grad for n, p in m.named_parameters()})
+            # (b) the loop
+            torch.manual_seed(77)
+            tl = DataLoader(CEOFirmDataset(data), batch_size=128, shuffle=True)
+            vl = DataLoader(CEOFirmDataset(data), batch_size=128, shuffle=False)
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf):
+                model = train_contrastive(tl, vl, meta, cfg, contrastive_weight=0.3, temperature=0.07,
+                                          use_triplet=trip)
+            out[f"{tag}/printed"] = np.array(buf.getvalue().splitlines())
+            put(out, f"{tag}/final", model.state_dict())
+    finally:
+        torch.nn.Dropout.__init__ = orig_dropout
+    np.savez_compressed(os.path.join(HERE, "contrastive_train.npz"), **out)
+    print("wrote contrastive_train.npz:", list(out["nce/printed"]), list(out["tri/printed"]))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["contrastive_train"]:
+        gen_contrastive_train()
+        sys.exit(0)
     if sys.argv[1:] == ["contrastive"]:
         gen_contrastive()
         sys.exit(0)
@@ -413,3 +482,4 @@ if __name__ == "__main__":
     gen_cli()
     gen_contrastive()
     gen_triplet()
+    gen_contrastive_train()

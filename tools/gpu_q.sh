@@ -1,3 +1,6 @@
+# quick GPU check: the named pytest files (default: every gpu test), one process, each test bounded
 set -o pipefail
 mkdir -p gpurun_out/q
-timeout -k 10 300 python -u -m pytest tests/test_gpu_contrastive.py -x -v --timeout 120 --timeout-method thread -k "semi_hard or info_nce_golden" > gpurun_out/q/t.log 2>&1; rc=$?; tail -25 gpurun_out/q/t.log; exit $rc
+FILES=${@:-tests}
+timeout -k 10 500 python -u -m pytest $FILES -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/q/t.log 2>&1; rc=$?
+grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/q/t.log | tail -60; [ $rc -eq 0 ] || tail -60 gpurun_out/q/t.log; exit $rc

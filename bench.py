@@ -41,6 +41,7 @@ CONFIGS = {
     "cfg2": (1_000_000, 32, 32, 64, 4096),
     "cfg3": (10_000_000, 64, 64, 128, 16384),
 }
+ACHIEVABLE_HBM_GBS = 6300.0  # MI355X_MICROARCH.md: float4 copy, 79 % of spec
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP32_TFLOPS = 157.3     # dense fp32 (vector == MFMA f32) spec
 # dense bf16 MFMA (v_mfma_f32_16x16x32_bf16: 16K flop / 16 cyc / SIMD, 1024 SIMDs,
@@ -175,7 +176,9 @@ def cosine_roofline(dev, D=128, n=1 << 22, reps=20):
     return {"kernel": "k_cosine<2,true>", "pairs": n, "D": D, "bytes_per_pair": 4 * (4 * D + 3),
             "avg_us": round(ms * 1e3, 2), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "stream_peak_measured": round(stream, 1),
-            "frac_of_measured_stream": round(gbs / stream, 4), "pairs_per_s": round(n / (ms * 1e-3), 1)}
+            "frac_of_measured_stream": round(gbs / stream, 4),
+            "achievable_hbm_guide": ACHIEVABLE_HBM_GBS, "frac_of_achievable": round(gbs / ACHIEVABLE_HBM_GBS, 4),
+            "pairs_per_s": round(n / (ms * 1e-3), 1)}
 
 
 def contrastive_cpu(D=256, B=4096):

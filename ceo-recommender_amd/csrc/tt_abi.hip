@@ -631,7 +631,8 @@ static int cosine_launch(const float* u, const float* v, const float* tg, const 
   if (!u || !v || !ls || !score || B < 0 || D <= 0) return TT_ERR_ARG;
   if (bwd && (!tg || !wt || !du || !dv || !loss || !dls)) return TT_ERR_ARG;
   if (B == 0) return TT_OK;
-  const int64_t rows_per_block = 256 / 16;
+  const bool vec0 = (D % 4 == 0);
+  const int64_t rows_per_block = vec0 ? COS_ROWS_PER_BLOCK : COS_ROWS_PER_BLOCK_ITER;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((B + rows_per_block - 1) / rows_per_block, 4096));
   const dim3 g(nb), t(256);
   const bool vec = (D % 4 == 0) && ((uintptr_t)u % 16 == 0) && ((uintptr_t)v % 16 == 0) &&

@@ -202,7 +202,8 @@ def contrastive_leg(dev, pg, world, rank, N=100_000, D=256, reps=3, cpu=False):
     matrix (N firms x N CEOs, D=256, L2-normalised synthetic embeddings),
     pairs sharded over the ranks (RCCL all-gather / all-reduce /
     reduce-scatter), plus retrieval ranks of every firm among all N CEOs."""
-    from ceo_firm_matching.contrastive import info_nce_loss, info_nce_loss_sharded, retrieval_ranks_rows
+    from ceo_firm_matching.contrastive import (info_nce_loss, info_nce_loss_sharded, retrieval_ranks_rows,
+                                               semi_hard_mining_rows)
     m = N // world
     g = torch.Generator(device=dev).manual_seed(500 + rank)
     f = torch.nn.functional.normalize(torch.randn(m, D, device=dev, generator=g), dim=1).requires_grad_(True)
@@ -240,10 +241,23 @@ def contrastive_leg(dev, pg, world, rank, N=100_000, D=256, reps=3, cpu=False):
             ranks = retrieval_ranks_rows(f.detach(), c_all, rank * m)
         torch.cuda.synchronize()
         tr = (time.perf_counter() - t1) / reps
+        # semi-hard negative mining (contrastive.py:141-192) of this rank's
+        # firms against all CEOs: the similarity GEMM + masked-min epilogue
+        semi_hard_mining_rows(f.detach(), c_all, rank * m, 0.2, N)
+        torch.cuda.synchronize()
+        if pg is not None:
+            dist.barrier()
+        t2 = time.perf_counter()
+        for _ in range(reps):
+            tri_loss, _, _ = semi_hard_mining_rows(f.detach(), c_all, rank * m, 0.2, N)
+        torch.cuda.synchronize()
+        tm = (time.perf_counter() - t2) / reps
+        if pg is not None:
+            dist.all_reduce(tri_loss)
     if pg is not None:
-        tt = torch.tensor([t, tr], device=dev, dtype=torch.float64)
+        tt = torch.tensor([t, tr, tm], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t, tr = tt.tolist()
+        t, tr, tm = tt.tolist()
     flops = 3 * 2.0 * N * N * D  # S, dF, dC GEMMs
     return {"workload": f"cfg5: InfoNCE fwd+bwd, {N} firms x {N} CEOs, D={D}, tau=0.07, fp32, "
                         f"pairs sharded over {world} GPU(s)",
@@ -253,6 +267,8 @@ def contrastive_leg(dev, pg, world, rank, N=100_000, D=256, reps=3, cpu=False):
             "frac": round(flops / t / 1e12 / (PEAK_BF16X3_TFLOPS * world), 4), "bound": "mfma",
             "loss": round(float(loss.detach()), 6),
             "retrieval_ranks_ms": round(tr * 1e3, 3), "ranks_median": float(ranks.float().median()),
+            "semi_hard_mining_ms": round(tm * 1e3, 3), "semi_hard_loss": round(float(tri_loss), 6),
+            "semi_hard_tflops": round(2.0 * N * N * D / tm / 1e12, 2),
             "cpu_baseline": contrastive_cpu(D) if cpu else None}
 
 

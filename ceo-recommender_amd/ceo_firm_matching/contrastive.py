@@ -38,7 +38,7 @@ from torch.utils.data import DataLoader
 
 from . import _native as N
 from .config import Config
-from .model import CEOFirmMatcher
+from .model import _POISON_WS, CEOFirmMatcher
 
 def _check_status(status: torch.Tensor):
     bad = int(status.item())
@@ -74,6 +74,8 @@ class _NCE:
         if self.ws_bytes < 0:
             N.check(self.ws_bytes, "tt_nce_workspace_bytes")
         self.ws = torch.empty(self.ws_bytes // 4, dtype=torch.float32, device=f.device)
+        if _POISON_WS:
+            self.ws.fill_(float("nan"))
         self.st = N.stream_ptr(f.device)
 
     def norms(self):
@@ -216,6 +218,8 @@ class _SemiHardFn(torch.autograd.Function):
         if wsb < 0:
             N.check(wsb, "tt_triplet_workspace_bytes")
         ws = torch.empty(wsb // 4, dtype=torch.float32, device=f.device)
+        if _POISON_WS:
+            ws.fill_(float("nan"))
         hardest = torch.empty(B, dtype=torch.int32, device=f.device)
         row_loss = torch.empty(B, dtype=torch.float32, device=f.device)
         loss = torch.zeros(1, dtype=torch.float32, device=f.device)
@@ -240,6 +244,31 @@ class _SemiHardFn(torch.autograd.Function):
                                             N.stream_ptr(f32.device)), "tt_triplet_backward")
         fd, cd, d_in = ctx.meta
         return df[:, :d_in].to(fd), dc[:, :d_in].to(cd), None
+
+
+def semi_hard_mining_rows(f: torch.Tensor, c: torch.Tensor, row0: int = 0, margin: float = 0.2,
+                          batch: Optional[int] = None):
+    """Forward mining for a row shard (no autograd): firm rows f [m, D] are
+    global rows row0.., ``c`` holds every CEO row [n, D].  Returns this
+    shard's loss share (sum of its row losses / batch), the hardest column
+    and the loss of each row."""
+    m, n = f.shape[0], c.shape[0]
+    if row0 < 0 or row0 + m > n:
+        raise ValueError("semi_hard_mining_rows: firm rows must map onto ceo rows row0..row0+m")
+    f32, c32 = _f32_pad4(f), _f32_pad4(c)
+    d = f32.shape[1]
+    L = N.lib()
+    wsb = int(L.tt_triplet_workspace_bytes(m, n, d))
+    if wsb < 0:
+        N.check(wsb, "tt_triplet_workspace_bytes")
+    ws = torch.empty(wsb // 4, dtype=torch.float32, device=f.device)
+    hardest = torch.empty(m, dtype=torch.int32, device=f.device)
+    row_loss = torch.empty(m, dtype=torch.float32, device=f.device)
+    loss = torch.zeros(1, dtype=torch.float32, device=f.device)
+    N.check(L.tt_triplet_forward(f32.data_ptr(), c32.data_ptr(), m, n, d, int(row0), ctypes.c_float(margin),
+                                 int(batch if batch is not None else n), ws.data_ptr(), wsb, hardest.data_ptr(),
+                                 row_loss.data_ptr(), loss.data_ptr(), N.stream_ptr(f.device)), "tt_triplet_forward")
+    return loss.reshape(()), hardest, row_loss
 
 
 def semi_hard_mining(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, margin: float = 0.2):

@@ -189,6 +189,9 @@ class CEOFirmMatcher(nn.Module):
         return (u * v).sum(dim=1, keepdim=True) * self.logit_scale.exp()
 
 
+_POISON_WS = bool(os.environ.get("CEO_TT_POISON_WS"))  # diagnostic: NaN-fill workspaces
+
+
 def _as_f32(x, dev):
     x = x.to(device=dev, dtype=torch.float32)
     return x if x.is_contiguous() else x.contiguous()
@@ -264,6 +267,8 @@ class _FusedTowerEmbeddings(torch.autograd.Function):
         train = bool(model.training)
         ws_bytes = N.workspace_bytes(arena.desc, max(B, 1))
         ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=f_num.device)
+        if _POISON_WS:
+            ws.fill_(float("nan"))
         emb = torch.empty(2, B, D, dtype=torch.float32, device=f_num.device)
         seed, step = model.next_dropout_stream() if train else (0, 0)
         batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
@@ -302,7 +307,6 @@ class _FusedTowerEmbeddings(torch.autograd.Function):
         return (None, None, None, None, None, *grads)
 
 
-_POISON_WS = bool(os.environ.get("CEO_TT_POISON_WS"))
 
 
 def _fused_inputs(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):

@@ -267,3 +267,20 @@ def test_semi_hard_matches_aten_reference_expression():
     a = semi_hard_negative_mining(f.to(dev), c.to(dev))
     b = semi_hard_negative_mining(f, c)
     assert abs(float(a) - float(b)) <= TOL * max(1.0, float(b))
+
+
+def test_semi_hard_row_shards_compose():
+    """Row shards against all CEO rows (the multi-GPU decomposition, as
+    bench.py's cfg-5 leg runs it) reproduce the single-launch mining."""
+    from ceo_firm_matching.contrastive import semi_hard_mining, semi_hard_mining_rows
+    dev = _dev()
+    gen = torch.Generator().manual_seed(21)
+    B, D, W = 3000, 64, 4
+    f = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1).to(dev)
+    c = torch.nn.functional.normalize(torch.randn(B, D, generator=gen) + 0.5 * f.cpu(), dim=1).to(dev)
+    loss, hardest, row_loss = semi_hard_mining(f, c)
+    m = B // W
+    parts = [semi_hard_mining_rows(f[r * m:(r + 1) * m], c, r * m, 0.2, B) for r in range(W)]
+    assert torch.equal(torch.cat([p[1] for p in parts]), hardest)
+    assert torch.equal(torch.cat([p[2] for p in parts]), row_loss)
+    assert abs(float(sum(p[0] for p in parts)) - float(loss.detach())) <= TOL * float(loss.detach())

@@ -259,23 +259,30 @@ int main() {
     timeit(nm, [&] { hipLaunchKernelGGL((k_cos2<LPR, RPG, PF>), dim3(GRID), dim3(256), 0, 0, U, V, T, W, B, D, s, ib, S, dU, dV, L); }); \
     check(nm);                                                                                                \
   }
-  RUN(2, 1, true, true, 4096)
-  RUN(2, 2, true, true, 4096)
-  RUN(2, 2, true, true, 8192)
-  RUN(2, 2, true, true, 16384)
-  RUN(2, 3, true, true, 4096)
-  RUN2(16, 2, false, 4096)
   RUN2(16, 2, true, 4096)
-  RUN2(16, 2, true, 2048)
-  RUN2(16, 1, true, 4096)
-  RUN2(16, 1, true, 8192)
-  RUN2(8, 1, false, 4096)
-  RUN2(8, 1, true, 4096)
-  RUN2(8, 2, false, 4096)
-  RUN2(8, 2, true, 2048)
-  RUN2(8, 2, true, 4096)
-  RUN2(16, 2, true, 1024)
-  RUN2(16, 3, false, 4096)
+  RUN2(16, 2, true, 4096)
+  // placement: the four streams in one pool, stream k at k * (nbytes + delta)
+  {
+    char* pool;
+    const size_t slack = (size_t)64 << 20;
+    CK(hipMalloc(&pool, 4 * (nbytes + slack)));
+    for (size_t delta : {(size_t)0, (size_t)256, (size_t)4096, (size_t)65536, (size_t)1 << 20, ((size_t)2 << 20) + 4096,
+                         (size_t)5 << 20, ((size_t)13 << 20) + 8192}) {
+      float* u2 = (float*)(pool);
+      float* v2 = (float*)(pool + 1 * (nbytes + delta));
+      float* du2 = (float*)(pool + 2 * (nbytes + delta));
+      float* dv2 = (float*)(pool + 3 * (nbytes + delta));
+      CK(hipMemcpy(u2, U, nbytes, hipMemcpyDeviceToDevice));
+      CK(hipMemcpy(v2, V, nbytes, hipMemcpyDeviceToDevice));
+      char nm[96];
+      snprintf(nm, 96, "cos2 pooled delta=%zu", delta);
+      timeit(nm, [&] { hipLaunchKernelGGL((k_cos2<16, 2, true>), dim3(4096), dim3(256), 0, 0, u2, v2, T, W, B, D, s, ib, S, du2, dv2, L); });
+      snprintf(nm, 96, "copy2 pooled delta=%zu", delta);
+      timeit(nm, [&] { hipLaunchKernelGGL((k_copy2<true>), dim3(8192), dim3(256), 0, 0, (f32x4*)u2, (f32x4*)v2, (f32x4*)du2, (f32x4*)dv2, B * D / 4); });
+    }
+    CK(hipFree(pool));
+  }
+  printf("U %p V %p dU %p dV %p\n", (void*)U, (void*)V, (void*)dU, (void*)dV);
   printf("done\n");
   return 0;
 }

@@ -298,6 +298,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / cosine legs")
+    ap.add_argument("--no-contrastive", action="store_true", help="skip the cfg-5 contrastive leg")
     ap.add_argument("--dp", action="store_true",
                     help="data-parallel step (all-reduce + Adam) even at world size 1 (tests the N>1 path)")
     args = ap.parse_args()
@@ -468,8 +469,9 @@ def main():
         del tr, model, data, rows
         graph = None
         torch.cuda.empty_cache()
-        result["contrastive"] = contrastive_leg(dev, pg, world, rank,
-                                                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
+        if not args.no_contrastive:
+            result["contrastive"] = contrastive_leg(dev, pg, world, rank,
+                                                    cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(nf, nc, D, B)

@@ -125,6 +125,16 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// 16-B write-through store (buffer_store_dwordx4 ... sc1): the line leaves the
+// XCD's L2 at once and is dropped there, so the kernel ends with no dirty
+// lines for the boundary's L2 write-back (MI355X_MICROARCH.md 'boundary':
+// + B / 6 TB/s when a kernel leaves B bytes dirty).  base must be uniform
+// across the wave (it becomes the SGPR buffer descriptor); off = per-lane bytes.
+__device__ __forceinline__ void st_wt16(const float* base, uint32_t off, f32x4 v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (int)off, 0, 16);
+}
+
 __device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
 __device__ __forceinline__ float bf16_val(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)

@@ -928,9 +928,9 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     sg[e] = dy[e] * ((z4s[e] - cf[h]) * cf[3 * H1 + h]);
   }
   {
-    float4* py = reinterpret_cast<float4*>(T.dY1 + row * H1 + 8 * g);
-    py[0] = make_float4(dy[0], dy[1], dy[2], dy[3]);
-    py[1] = make_float4(dy[4], dy[5], dy[6], dy[7]);
+    const uint32_t off = (uint32_t)((row * H1 + 8 * g) * 4);
+    st_wt16(T.dY1, off, f32x4{dy[0], dy[1], dy[2], dy[3]});
+    st_wt16(T.dY1, off + 16, f32x4{dy[4], dy[5], dy[6], dy[7]});
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -979,7 +979,7 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     const int d = 16 * pt + r;
     if (d < D) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) *reinterpret_cast<f32x4*>(slab + T.so_W8 + d * H1 + 16 * q + 4 * g) = acc[q];
+      for (int q = 0; q < 2; ++q) st_wt16(slab, (uint32_t)((T.so_W8 + d * H1 + 16 * q + 4 * g) * 4), acc[q]);
       if (g == 0) slab[T.so_b8 + d] = accb[0];
     }
   }

@@ -234,6 +234,31 @@ __device__ __forceinline__ float xrow32_add(float v) {  // v[l] + v[l ^ 32]
   const unsigned lo = p[0], hi = p[1];
   return __uint_as_float(lo) + __uint_as_float(hi);
 }
+// 4x4 transpose inside each lane quad (lanes 4c..4c+3): on entry lane k
+// holds column k of the quad's 4x4 block (v[i] = M[i][k]), on exit row k
+// (M[k][0..3]).  Two DPP exchange stages (xor 2, xor 1), no LDS.
+__device__ __forceinline__ f32x4 quad_transpose(f32x4 v) {
+  const int k = lane_id() & 3;
+  const bool hi = (k & 2) != 0, odd = (k & 1) != 0;
+  float a0 = hi ? v[0] : v[2], a1 = hi ? v[1] : v[3];
+  float b0 = dpp_mov<0x4E>(a0), b1 = dpp_mov<0x4E>(a1);  // quad_perm [2,3,0,1]
+  const f32x4 s = hi ? f32x4{b0, b1, v[2], v[3]} : f32x4{v[0], v[1], b0, b1};
+  a0 = odd ? s[0] : s[1];
+  a1 = odd ? s[2] : s[3];
+  b0 = dpp_mov<0xB1>(a0);  // quad_perm [1,0,3,2]
+  b1 = dpp_mov<0xB1>(a1);
+  return odd ? f32x4{b0, s[1], b1, s[3]} : f32x4{s[0], b0, s[2], b1};
+}
+// Store a 16x16 tile held in the MFMA accumulator layout (lane (r, g): rows
+// 4g..4g+3 of column r) row-major: quad transpose, then one 16-B
+// write-through store per lane (4 consecutive columns of one row).
+// base: block-uniform pointer; off: element offset of the tile's (0, 0) from
+// base (small); ld: row stride in floats (multiple of 4, base 16-B aligned).
+__device__ __forceinline__ void store_tile_rm_wt(const float* base, int off, int ld, f32x4 acc) {
+  const int l = lane_id(), r = l & 15, g = l >> 4;
+  const f32x4 t = quad_transpose(acc);
+  st_wt16(base, (uint32_t)((off + (4 * g + (r & 3)) * ld + (r & ~3)) * 4), t);
+}
 // sum over the 4 lane groups (g = l>>4) that share a column r
 __device__ __forceinline__ float col_reduce(float v) { return xrow32_add(xrow16_add(v)); }
 // sum over the 16 lanes (r) that share a row group g

@@ -427,11 +427,10 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
     cols_to_lds<4>(s1, red);
     cols_to_lds<4>(s2, red + H0);
   }
-  // Z0 (workspace rows are padded to whole tiles: no guard)
+  // Z0 (workspace rows are padded to whole tiles: no guard), row-major via
+  // quad transposes, 16-B write-through stores
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) T.Z0[(r0 + 16 * w + 4 * g + i) * H0 + 16 * j + r] = acc[j][i];
+  for (int j = 0; j < 4; ++j) store_tile_rm_wt(T.Z0 + r0 * H0, 16 * w * H0 + 16 * j, H0, acc[j]);
   if (t == 0 && a.target && threadIdx.x < R) {  // (target, weight) of the tile's rows for k_top
     const int64_t drt = data_row(a, base, min(r0 + (int64_t)threadIdx.x, a.B - 1));
     *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + threadIdx.x)) = make_float2(a.target[drt], a.weight[drt]);
@@ -556,9 +555,7 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
     cols_to_lds<2>(s2, red + H1);
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) T.Z4[(r0 + 16 * w + 4 * g + i) * H1 + 16 * j + r] = acc[j][i];
+  for (int j = 0; j < 2; ++j) store_tile_rm_wt(T.Z4 + r0 * H1, 16 * w * H1 + 16 * j, H1, acc[j]);
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H1) atomicAdd(&T.st1[rep_of_block() * 2 * H1 + threadIdx.x], red[threadIdx.x]);
@@ -1117,9 +1114,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     f32x4 acc[2] = {zero4(), zero4()};
     strip_gemm_nt<2>(dZT + 16 * p * LDT, LDT, A0T + 16 * q0 * LDT, LDT, R, acc);
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) slab[T.so_W4 + (16 * p + 4 * g + i) * H0 + 16 * (q0 + q) + r] = acc[q][i];
+    for (int q = 0; q < 2; ++q) store_tile_rm_wt(slab, (int)T.so_W4 + 16 * p * H0 + 16 * (q0 + q), H0, acc[q]);
   }
 
   // dA0 = dZ4 W4  (K = 32; A from the transposed image, W4 row-major)
@@ -1129,16 +1124,17 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   float sg[4], sb[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = 16 * j + r;
     sg[j] = 0.f;
     sb[j] = 0.f;
+    f32x4 dyv;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float dy = a0[j][i] > 0.f ? dA[j][i] * scl : 0.f;  // 0 on rows >= B (a0 = 0)
-      T.dY0[(r0 + 16 * w + 4 * g + i) * H0 + col] = dy;
+      dyv[i] = dy;
       sg[j] += dy * zh0[j][i];
       sb[j] += dy;
     }
+    store_tile_rm_wt(T.dY0 + r0 * H0, 16 * w * H0 + 16 * j, H0, dyv);
   }
   cols_to_lds<4>(sg, red);
   cols_to_lds<4>(sb, red + H0);
@@ -1303,10 +1299,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   // every input column tile; results go straight into this tile's slab
   float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
   const int in = T.in_dim;
+  const bool w0_vec = (in & 3) == 0 && (T.so_W0 & 3) == 0;
   auto put_w0 = [&](int kt, const f32x4& acc) {
     const int k = 16 * kt + r;
     float* dst = slab + T.so_W0 + (16 * w + 4 * g) * in + k;
-    if (16 * kt + 16 <= in) {
+    if (w0_vec && 16 * kt + 16 <= in) {  // whole tile: row-major 16-B write-through stores
+      store_tile_rm_wt(slab, (int)T.so_W0 + 16 * w * in + 16 * kt, in, acc);
+    } else if (16 * kt + 16 <= in) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) dst[i * in] = acc[i];
     } else if (k < in) {

@@ -342,6 +342,8 @@ def main():
     n_batches = shard // B
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     rows = torch.randperm(shard, device=dev, generator=gen)
+    if os.environ.get("CEO_BENCH_SEQ_ROWS"):  # diagnostic: in-order rows (gather locality probe)
+        rows = torch.arange(shard, device=dev)
 
     # hipGraph replay of whole steps at every world size: the RCCL all-reduce
     # of the data-parallel step is captured with the kernels (no host work

@@ -43,10 +43,26 @@ constexpr float SUM_MIN = 1e-30f;  // row/col sums below this: exp underflow (re
 // 16 cycles per 32-deep K step instead of 8 fp32 MFMAs of 32 cycles (2.7x).
 // The split happens once per element while staging into LDS.
 constexpr int NPL = 3;                // planes h, m, l
-constexpr int LDK = BK + 8;           // bf16 per LDS row (80 B: 16-B aligned rows)
-constexpr int PLANE = BM * LDK;       // bf16 per plane of one operand (BM == BN)
-constexpr int OPND = NPL * PLANE;     // bf16 per operand
-constexpr size_t LDS_BYTES = sizeof(uint16_t) * 2 * OPND;  // A + B, single buffer (120 KB)
+// LDS operand images [plane][m][k] bf16, two layouts:
+//  * SWZ (both operands row-major along k, the similarity kernels): 64-B rows,
+//    16-B granule c of row m stored at c ^ swz(m), swz = [0,2,3,1][(m >> 2) & 3]:
+//    every 16-lane group of a ds_read_b128 fragment read (rows r, granule g)
+//    hits 16 distinct 16-B slots of the 256-B bank window (MI355X_MICROARCH.md
+//    LDS table) -- conflict-free reads and row-contiguous staging writes;
+//  * padded (the gradient kernels, whose k-major staging writes 16 rows at one
+//    k): 80-B rows.
+template <bool SWZ> struct Lay {
+  static constexpr int LDK = SWZ ? BK : BK + 8;  // bf16 per LDS row
+  static constexpr int PLANE = BM * LDK;         // bf16 per plane of one operand (BM == BN)
+  static constexpr int OPND = NPL * PLANE;       // bf16 per operand
+};
+__device__ __forceinline__ int lds_swz(int m) { return (0x78 >> (2 * ((m >> 2) & 3))) & 3; }
+template <bool SWZ>
+__device__ __forceinline__ int lds_off(int m, int k) {  // bf16 offset of (m, k) in a plane
+  if constexpr (SWZ) return m * Lay<SWZ>::LDK + ((((k >> 3) ^ lds_swz(m)) << 3) | (k & 7));
+  else return m * Lay<SWZ>::LDK + k;
+}
+constexpr size_t LDS_BYTES = sizeof(uint16_t) * 2 * Lay<false>::OPND;  // A + B, single buffer (120 KB max)
 
 
 // Where an operand comes from.  LDS always holds [m][k] bf16 planes.
@@ -203,8 +219,9 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
 }
 
 // split the staged float4s into the three bf16 planes of LDS [m][k]
-template <int S>
+template <int S, bool SWZ>
 __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[4]) {
+  constexpr int PLANE = Lay<SWZ>::PLANE;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int e = (int)threadIdx.x + q * NTH;
@@ -220,7 +237,7 @@ __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[4]) {
     uint32_t h01, m01, l01, h23, m23, l23;  // packed bf16 pairs of the three planes
     split3x2(v[q].x, v[q].y, h01, m01, l01);
     split3x2(v[q].z, v[q].w, h23, m23, l23);
-    uint16_t* d = L + m * LDK + k;  // one 8-byte write per plane
+    uint16_t* d = L + lds_off<SWZ>(m, k);  // one 8-byte write per plane
     *reinterpret_cast<uint2*>(d) = make_uint2(h01, h23);
     *reinterpret_cast<uint2*>(d + PLANE) = make_uint2(m01, m23);
     *reinterpret_cast<uint2*>(d + 2 * PLANE) = make_uint2(l01, l23);
@@ -228,8 +245,9 @@ __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[4]) {
 }
 
 // MFMA operand: 8 consecutive k (k = kk + 8g .. +7) of row m, one plane
+template <bool SWZ>
 __device__ __forceinline__ bf16x8 frag(const uint16_t* L, int plane, int m, int g) {
-  return *reinterpret_cast<const bf16x8*>(L + plane * PLANE + m * LDK + 8 * g);
+  return *reinterpret_cast<const bf16x8*>(L + plane * Lay<SWZ>::PLANE + lds_off<SWZ>(m, 8 * g));
 }
 
 
@@ -248,14 +266,15 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
   float4 va[4], vb[4];
   const int nch = (int)((ke - kb + BK - 1) / BK);
   if (nch <= 0) return;
+  constexpr bool SWZ = SA == SRC_MK && SB == SRC_MK;
   uint16_t* As = smem;
-  uint16_t* Bs = smem + OPND;
+  uint16_t* Bs = smem + Lay<SWZ>::OPND;
   load_opnd<SA>(g_.A, m0, kb, va);
   load_opnd<SB>(g_.B, n0, kb, vb);
   for (int c = 0; c < nch; ++c) {
     __syncthreads();  // the previous chunk's fragments have been read
-    store_opnd<SA>(As, va);
-    store_opnd<SB>(Bs, vb);
+    store_opnd<SA, SWZ>(As, va);
+    store_opnd<SB, SWZ>(Bs, vb);
     __syncthreads();
     if (c + 1 < nch) {
       load_opnd<SA>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
@@ -265,12 +284,12 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int p = 0; p < NPL; ++p) a[i][p] = frag(As, p, wm * WM + 16 * i + r, g);
+      for (int p = 0; p < NPL; ++p) a[i][p] = frag<SWZ>(As, p, wm * WM + 16 * i + r, g);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bf16x8 b[NPL];
 #pragma unroll
-      for (int p = 0; p < NPL; ++p) b[p] = frag(Bs, p, wn * WN + 16 * j + r, g);
+      for (int p = 0; p < NPL; ++p) b[p] = frag<SWZ>(Bs, p, wn * WN + 16 * j + r, g);
 #pragma unroll
       for (int q = 0; q < 6; ++q)
 #pragma unroll

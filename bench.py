@@ -181,6 +181,54 @@ def cosine_roofline(dev, D=128, n=1 << 22, reps=20):
             "pairs_per_s": round(n / (ms * 1e-3), 1)}
 
 
+def side_config_leg(dev, name, steps=200, warmup=20):
+    """Single-GPU pairs/s of another BASELINE config (graph-replayed fused
+    steps over its own synthetic dataset) -- reported beside the headline
+    workload, not as `value`."""
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    from ceo_firm_matching.engine import FusedTrainer
+    from ceo_firm_matching.synthetic import generate_pairs
+    n_total, nf, nc, D, B = CONFIGS[name]
+    data = generate_pairs(n_total, nf, nc, seed=42, device=dev)
+    meta = {k: data[k] for k in ("n_firm_numeric", "firm_cat_counts", "n_ceo_numeric", "ceo_cat_counts")}
+    cfg = Config()
+    cfg.LATENT_DIM = D
+    cfg.DEVICE = dev
+    torch.manual_seed(42)
+    model = CEOFirmMatcher(meta, cfg).to(dev)
+    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42)
+    tr.set_data(data)
+    n_batches = n_total // B
+    rows = torch.randperm(n_total, device=dev, generator=torch.Generator(device=dev).manual_seed(1000))
+    for _ in range(warmup):
+        tr.step_cycle(rows, B, n_batches)
+    chunk = 10
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            tr.step_cycle(rows, B, n_batches)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(chunk):
+            tr.step_cycle(rows, B, n_batches)
+    graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps // chunk):
+        graph.replay()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    n = (steps // chunk) * chunk
+    out = {"workload": f"{name}: {n_total} pairs, {nf}x{nc} feats, LATENT={D}, bs={B}, 1 GPU, hipGraph",
+           "value": round(n * B / t, 1), "unit": "pairs/s", "ms_per_step": round(1e3 * t / n, 4)}
+    del graph, tr, model, data, rows
+    torch.cuda.empty_cache()
+    return out
+
+
 def contrastive_cpu(D=256, B=4096):
     """CPU oracle InfoNCE fwd+bwd (the reference's info_nce_loss algebra) at
     B=4096, extrapolated to N x N pairs (work grows as B^2)."""
@@ -467,6 +515,9 @@ def main():
         result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)
         if rank == 0:
             result["cosine_roofline"] = cosine_roofline(dev, D=D)
+        if world == 1:  # the other single-GPU BASELINE config (cfg 2), beside the headline one
+            others = [c for c in CONFIGS if c != args.config]
+            result["other_configs"] = {c: side_config_leg(dev, c) for c in others}
         # drop the training state before the 40 GB (N=1) similarity workspace
         del tr, model, data, rows
         graph = None

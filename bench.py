@@ -467,7 +467,11 @@ def main():
         "config": {"workload": f"{args.config}: {n_total} pairs ({shard}/GPU), {nf}x{nc} feats, LATENT={D}, "
                                f"bs={B}/GPU, dropout 0.1, Adam lr 4e-4",
                    "global_batch": B * world, "parallelism": f"dp{world}" if pg is not None else "single",
-                   "graph": bool(graph is not None), "graph_chunk": chunk},
+                   "graph": bool(graph is not None), "graph_chunk": chunk,
+                   "grad_exchange": ("peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
+                                     else ("rccl all-reduce" if pg is not None and dist.get_backend(pg) == "nccl"
+                                           else ("gloo all-reduce" if pg is not None else "none"))),
+                   "exchange_vs_collective_us": (getattr(getattr(tr, "peer", None), "timing_us", None))},
         "mean_loss": round(loss, 5),
     }
 

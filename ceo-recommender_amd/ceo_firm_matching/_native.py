@@ -61,6 +61,14 @@ class TTAdamHP(ctypes.Structure):
                 ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
 
 
+TT_AR_MAX_RANKS = 16
+TT_AR_HANDLE_BYTES = 64
+
+
+class TTArPeers(ctypes.Structure):  # tt_ar_peers
+    _fields_ = [("region", ctypes.c_void_p * TT_AR_MAX_RANKS)]
+
+
 _LIB: Optional[ctypes.CDLL] = None
 
 
@@ -104,6 +112,13 @@ def lib() -> ctypes.CDLL:
         "tt_nce_backward": (I32, [P, P, I64, I64, I32, I64, I64, F, P, I64, P, P, P]),
         "tt_rank_workspace_bytes": (I64, [I64]),
         "tt_retrieval_ranks": (I32, [P, P, I64, I64, I32, I64, P, I64, P, P]),
+        "tt_ar_region_bytes": (I64, [I64]),
+        "tt_ar_alloc": (I32, [I64, ctypes.POINTER(P), P]),
+        "tt_ar_open": (I32, [P, ctypes.POINTER(P)]),
+        "tt_ar_close": (I32, [P]),
+        "tt_ar_free": (I32, [P]),
+        "tt_ar_reset": (I32, [P, I64, P]),
+        "tt_ar_allreduce_adam": (I32, [ctypes.POINTER(TTArPeers), I32, I32, I64, P, P, P, P, P, H, P, I64, P, P]),
         "tt_triplet_workspace_bytes": (I64, [I64, I64, I32]),
         "tt_triplet_forward": (I32, [P, P, I64, I64, I32, I64, F, I64, P, I64, P, P, P, P]),
         "tt_triplet_backward": (I32, [P, P, I64, I64, I32, I64, I64, P, P, P, P, P, P]),

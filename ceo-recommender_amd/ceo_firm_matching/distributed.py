@@ -10,10 +10,14 @@ rank 0's state at construction: ``broadcast_state_``).
 """
 from __future__ import annotations
 
+import ctypes
+import time
 from typing import Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+from . import _native as N
 
 
 def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -51,3 +55,152 @@ def broadcast_state_(params: torch.Tensor, buffers: Optional[torch.Tensor] = Non
         dist.broadcast(params, src=src, group=group)
         if buffers is not None:
             dist.broadcast(buffers, src=src, group=group)
+
+
+class PeerExchange:
+    """One-shot gradient exchange + Adam over peer memory (tt_ar_*), the
+    data-parallel step's only collective done in ONE launch instead of an
+    RCCL all-reduce followed by an Adam kernel.
+
+    ``create`` maps every rank's exchange region (IPC handles all-gathered
+    over ``group``), checks the exchange against ``all_reduce`` on random
+    gradients, times both, and returns None -- the caller keeps the
+    collective -- unless every rank agrees the exchange is correct and faster.
+    ``CEO_TT_PEER_AR=0`` disables it, ``=1`` skips the timing comparison."""
+
+    def __init__(self, lib, regions, own, rank, world, n, device):
+        self.lib, self.rank, self.world, self.n, self.device = lib, rank, world, n, device
+        self.regions, self.own = regions, own
+        self.peers = N.TTArPeers()
+        for q, r in enumerate(regions):
+            self.peers.region[q] = r
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.epoch = 0  # host epochs of the setup checks (before reset)
+        self.timing_us = None  # (exchange, collective) per step, measured by create()
+
+    @staticmethod
+    def create(n: int, group=None, device=None, mode: Optional[str] = None) -> "Optional[PeerExchange]":
+        import os
+        mode = os.environ.get("CEO_TT_PEER_AR", "auto") if mode is None else mode
+        world = world_of(group)
+        if mode == "0" or world < 2 or world > N.TT_AR_MAX_RANKS:
+            return None
+        rank = dist.get_rank(group)
+        flag_dev = device if dist.get_backend(group) == "nccl" else "cpu"
+        ok = torch.ones(1, dtype=torch.int32, device=flag_dev)
+        ex = None
+        try:
+            ex = PeerExchange._map(n, group, device, rank, world)
+        except Exception:  # noqa: BLE001 -- any setup failure keeps the collective
+            ok.zero_()
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # every rank mapped, or none uses it
+        if int(ok.item()) == 0:
+            if ex is not None:
+                ex.close()
+            return None
+        use = torch.ones(1, dtype=torch.int32, device=flag_dev)
+        try:
+            if not ex._check(group):
+                use.zero_()
+            elif mode != "1" and not ex._faster_than_collective(group):
+                use.zero_()
+        except Exception:  # noqa: BLE001
+            use.zero_()
+        dist.all_reduce(use, op=dist.ReduceOp.MIN, group=group)
+        if int(use.item()) == 0:
+            ex.close()
+            return None
+        ex.reset(group)
+        return ex
+
+    @staticmethod
+    def _map(n, group, device, rank, world):
+        lib = N.lib()
+        nbytes = int(lib.tt_ar_region_bytes(n))
+        own = ctypes.c_void_p()
+        handle = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)()
+        N.check(lib.tt_ar_alloc(nbytes, ctypes.byref(own), handle), "tt_ar_alloc")
+        mine = torch.tensor(list(bytes(handle)), dtype=torch.uint8)
+        if dist.get_backend(group) == "nccl":
+            mine = mine.to(device)
+        allh = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allh, mine, group=group)
+        regions = []
+        for q in range(world):
+            if q == rank:
+                regions.append(own.value)
+                continue
+            h = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)(*allh[q].cpu().tolist())
+            p = ctypes.c_void_p()
+            N.check(lib.tt_ar_open(h, ctypes.byref(p)), "tt_ar_open")
+            regions.append(p.value)
+        return PeerExchange(lib, regions, own.value, rank, world, n, device)
+
+    def close(self):
+        for q, r in enumerate(self.regions):
+            if r and q != self.rank:
+                self.lib.tt_ar_close(ctypes.c_void_p(r))
+        if self.own:
+            self.lib.tt_ar_free(ctypes.c_void_p(self.own))
+        self.regions, self.own = [], None
+
+    def reset(self, group=None):
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)  # every rank done with its setup exchanges
+        N.check(self.lib.tt_ar_reset(ctypes.c_void_p(self.own), self.n, N.stream_ptr(self.device)), "tt_ar_reset")
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)  # every region zeroed before any rank publishes epoch 1
+        self.err.zero_()
+        self.epoch = 0
+
+    def run(self, grad, grad_out=None, params=None, exp_avg=None, exp_avg_sq=None, hp=None, state=None,
+            step_host: int = 0):
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        rc = self.lib.tt_ar_allreduce_adam(ctypes.byref(self.peers), self.rank, self.world, self.n,
+                                           grad.data_ptr(), ptr(grad_out), ptr(params), ptr(exp_avg),
+                                           ptr(exp_avg_sq), hp, ptr(state), int(step_host), self.err.data_ptr(),
+                                           N.stream_ptr(self.device))
+        N.check(rc, "tt_ar_allreduce_adam")
+
+    def _check(self, group) -> bool:
+        g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)
+        good = True
+        for _ in range(3):
+            x = torch.randn(self.n, device=self.device, generator=g)
+            out = torch.empty_like(x)
+            self.epoch += 1
+            self.run(x, grad_out=out, step_host=self.epoch)
+            ref = x.clone()
+            dist.all_reduce(ref, group=group)
+            ref /= self.world
+            torch.cuda.synchronize(self.device)
+            if int(self.err.item()) != 0:
+                return False
+            good &= bool(torch.allclose(out, ref, rtol=1e-5, atol=1e-6))
+        return good
+
+    def _faster_than_collective(self, group, reps: int = 20) -> bool:
+        x = torch.randn(self.n, device=self.device)
+        out = torch.empty_like(x)
+
+        def timed(fn):
+            fn()
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=group)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize(self.device)
+            return (time.perf_counter() - t0) / reps
+
+        def mine():
+            self.epoch += 1
+            self.run(x, grad_out=out, step_host=self.epoch)
+
+        t_ex = timed(mine)
+        t_cc = timed(lambda: average_gradients_(out, group))
+        dev = self.device if dist.get_backend(group) == "nccl" else "cpu"
+        tt = torch.tensor([t_ex, t_cc], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+        self.timing_us = (1e6 * float(tt[0]), 1e6 * float(tt[1]))
+        return int(self.err.item()) == 0 and float(tt[0]) < float(tt[1])

@@ -19,7 +19,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _native as N
-from .distributed import average_gradients_, broadcast_state_, world_of
+from .distributed import PeerExchange, average_gradients_, broadcast_state_, world_of
 from .model import CEOFirmMatcher
 
 DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")
@@ -51,6 +51,9 @@ class FusedTrainer:
         self.world = world_of(process_group) if self.dp else 1
         if self.world > 1:  # DDP construction semantics: rank 0's state everywhere
             broadcast_state_(self.arena.params, self.arena.buffers, process_group)
+        # one-launch gradient exchange + Adam over peer memory when every rank
+        # can map it and it beats the collective (else the RCCL all-reduce)
+        self.peer = PeerExchange.create(n, process_group, dev) if self.world > 1 else None
         self.max_batch = 0
         self.ws = None
         self.ensure_batch(max_batch)
@@ -128,8 +131,12 @@ class FusedTrainer:
         self.steps_host += 1
 
     def allreduce_and_adam(self):
-        average_gradients_(self.grad, self.pg)
         a = self.arena
+        if self.peer is not None:  # mean over ranks + Adam, one launch
+            self.peer.run(self.grad, grad_out=self.grad, params=a.params, exp_avg=self.exp_avg,
+                          exp_avg_sq=self.exp_avg_sq, hp=self.hp, state=self.state)
+            return
+        average_gradients_(self.grad, self.pg)
         rc = self.lib.tt_adam_apply(a.params.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
                                     self.exp_avg_sq.data_ptr(), a.params.numel(), self.hp,
                                     self.state.data_ptr(), 0, N.stream_ptr(self.device))
@@ -144,6 +151,9 @@ class FusedTrainer:
         t = self.loss_sum_tensor()
         v = float(t.item()) if read else None
         t.zero_()
+        if read and self.peer is not None and int(self.peer.err.item()) != 0:
+            raise RuntimeError("peer gradient exchange: a rank did not publish within the wait bound "
+                               "(set CEO_TT_PEER_AR=0 to use the RCCL all-reduce)")
         return v
 
     def steps_done(self) -> int:

@@ -10,6 +10,7 @@
 #include "tt_common.h"
 #include "tt_tower.hip"
 #include "tt_optim.hip"
+#include "tt_comm.hip"
 #include "tt_cosine.hip"
 #include "tt_contrastive.hip"
 
@@ -974,6 +975,95 @@ int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n
   (void)hipMemsetAsync(dc, 0, sizeof(float) * n * d, s);
   hipLaunchKernelGGL(k_triplet_bwd, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s, f, c, m, d, row0, hardest,
                      row_loss, grad_loss, (float)(1.0 / (double)batch), df, dc);
+  return launch_check();
+}
+
+// ---- data-parallel gradient exchange over peer memory ----
+static constexpr int AR_BLOCKS = 32;
+static int64_t ar_flag_bytes() { return (int64_t)TT_AR_MAX_RANKS * AR_BLOCKS * 8; }
+static int64_t ar_slot_floats(int64_t n) { return (n + 63) / 64 * 64; }
+
+int64_t tt_ar_region_bytes(int64_t n) {
+  if (n < 1) return TT_ERR_ARG;
+  return ar_flag_bytes() + 2 * ar_slot_floats(n) * (int64_t)sizeof(float);
+}
+
+int32_t tt_ar_alloc(int64_t bytes, void** region, void* ipc_handle) {
+  if (bytes < 1 || !region || !ipc_handle) return TT_ERR_ARG;
+  static_assert(sizeof(hipIpcMemHandle_t) == TT_AR_HANDLE_BYTES, "IPC handle size");
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(p, 0, (size_t)bytes);
+  if (e == hipSuccess) {
+    hipIpcMemHandle_t h;
+    e = hipIpcGetMemHandle(&h, p);
+    if (e == hipSuccess) std::memcpy(ipc_handle, &h, sizeof(h));
+  }
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return (int)e;
+  }
+  *region = p;
+  return TT_OK;
+}
+
+int32_t tt_ar_open(const void* ipc_handle, void** region) {
+  if (!ipc_handle || !region) return TT_ERR_ARG;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, ipc_handle, sizeof(h));
+  void* p = nullptr;
+  const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) return (int)e;
+  *region = p;
+  return TT_OK;
+}
+
+int32_t tt_ar_close(void* region) { return region ? (int)hipIpcCloseMemHandle(region) : TT_ERR_ARG; }
+int32_t tt_ar_free(void* region) { return region ? (int)hipFree(region) : TT_ERR_ARG; }
+
+int32_t tt_ar_reset(void* region, int64_t n, tt_stream_t stream) {
+  if (!region || n < 1) return TT_ERR_ARG;
+  return (int)hipMemsetAsync(region, 0, (size_t)tt_ar_region_bytes(n), (hipStream_t)stream);
+}
+
+int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t world, int64_t n, const float* grad,
+                             float* grad_out, float* params, float* exp_avg, float* exp_avg_sq,
+                             const tt_adam_hp* hp, tt_state* state, int64_t step_host, int32_t* err,
+                             tt_stream_t stream) {
+  if (!peers || world < 1 || world > TT_AR_MAX_RANKS || rank < 0 || rank >= world || n < 1 || !grad || !err)
+    return TT_ERR_ARG;
+  if (params && (!exp_avg || !exp_avg_sq || !hp)) return TT_ERR_ARG;
+  if (!state && step_host < 1) return TT_ERR_ARG;
+  ArArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int q = 0; q < world; ++q) {
+    if (!peers->region[q]) return TT_ERR_ARG;
+    char* base = (char*)peers->region[q];
+    a.flags[q] = (uint64_t*)base;
+    a.slot[q] = (float*)(base + ar_flag_bytes());
+  }
+  a.slot_stride = ar_slot_floats(n);
+  a.rank = rank;
+  a.world = world;
+  a.blocks = AR_BLOCKS;
+  a.n = n;
+  a.grad = grad;
+  a.grad_out = grad_out;
+  a.p = params;
+  a.m = exp_avg;
+  a.v = exp_avg_sq;
+  if (hp) {
+    a.lr = hp->lr;
+    a.b1 = hp->beta1;
+    a.b2 = hp->beta2;
+    a.eps = hp->eps;
+  }
+  a.state = state;
+  a.step_host = step_host;
+  a.err = err;
+  a.spin_limit = 1u << 26;  // ~4 s of s_sleep(2) polling, then give up (err)
+  hipLaunchKernelGGL(k_ar_adam, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
   return launch_check();
 }
 

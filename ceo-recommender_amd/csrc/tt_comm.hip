@@ -1,0 +1,113 @@
+// Data-parallel gradient exchange over peer memory (xGMI), gfx950.
+//
+// The only exchange of the data-parallel step is the mean over
+// ranks of the 85 KB flat gradient, followed by Adam (training.py:55).  At
+// this size an all-reduce is pure latency; this is a one-shot exchange in ONE
+// launch that also applies Adam:
+//
+//   every rank owns an exchange region (uncached device memory, shared with the
+//   other ranks through IPC handles): two gradient slots (step parity) and a
+//   flag word per (source rank, block).  Block b of rank r
+//     1. copies slice b of its gradient into its own slot[t & 1],
+//     2. waits for those stores, then writes epoch t into flag[r][b] of every
+//        rank (remote stores over xGMI),
+//     3. waits (bounded) until flag[p][b] == t for every rank p,
+//     4. reads slice b of every rank's slot[t & 1] -- in rank order, so every
+//        rank computes bitwise the same mean -- scales by 1/world and applies
+//        Adam (the k_adam arithmetic) to its parameters.
+//   Slot reuse is safe: rank r rewrites slot[t & 1] at step t + 2, after its
+//   step-(t+1) exchange saw every peer's step-(t+1) flags, which each peer
+//   wrote after finishing its step-t reads (stream order).
+//   The epoch is the device step counter (tt_state.step_cur), so the launch
+//   replays unchanged inside a captured hipGraph.
+//   A wait that exceeds its bound sets *err and gives up (no hang); the host
+//   checks err and falls back to RCCL.
+#include "tt_common.h"
+
+namespace tt {
+
+constexpr int AR_THREADS = 256;
+
+struct ArArgs {
+  float* slot[TT_AR_MAX_RANKS];          // slot 0 of each rank's region (slot 1 at + slot_stride)
+  uint64_t* flags[TT_AR_MAX_RANKS];      // each rank's flag array [TT_AR_MAX_RANKS][blocks]
+  int64_t slot_stride;                   // floats between slot 0 and slot 1
+  int rank, world, blocks;
+  int64_t n;                             // gradient floats
+  const float* grad;                     // this rank's gradient (k_reduce_adam output)
+  float* grad_out;                       // mean gradient (nullable)
+  float *p, *m, *v;                      // Adam (nullable p: no Adam)
+  float lr, b1, b2, eps;
+  tt_state* state;
+  int64_t step_host;
+  int32_t* err;                          // set when a wait times out
+  uint32_t spin_limit;
+};
+
+__device__ __forceinline__ uint64_t ld_flag(const uint64_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
+  const int64_t t = a.state ? a.state->step_cur : a.step_host;
+  const uint64_t epoch = (uint64_t)t;
+  const int b = blockIdx.x;
+  const int64_t per = (a.n + a.blocks - 1) / a.blocks;
+  const int64_t lo = b * per, hi = min(a.n, lo + per);
+  const int64_t par = (t & 1) ? a.slot_stride : 0;
+  float* mine = a.slot[a.rank] + par;
+  // 1. publish this block's slice (system-coherent stores), every thread's
+  // stores performed before the barrier that precedes the flags
+  for (int64_t e = lo + threadIdx.x; e < hi; e += AR_THREADS)
+    __hip_atomic_store(mine + e, a.grad[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  // 2. signal every rank (one lane per destination)
+  if (threadIdx.x < a.world) {
+    uint64_t* f = a.flags[threadIdx.x] + (int64_t)a.rank * a.blocks + b;
+    __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 3. wait for every rank's slice b (bounded)
+  __shared__ int ok_s;
+  if (threadIdx.x == 0) ok_s = 1;
+  __syncthreads();
+  if (threadIdx.x < a.world) {
+    const uint64_t* f = a.flags[a.rank] + (int64_t)threadIdx.x * a.blocks + b;
+    uint32_t k = 0;
+    while (ld_flag(f) < epoch) {
+      if (++k > a.spin_limit) {
+        ok_s = 0;
+        atomicAdd(a.err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  const bool ok = ok_s != 0;
+  // 4. mean over ranks in rank order + Adam
+  const float inv_w = 1.0f / (float)a.world;
+  AdamCoef c;
+  if (a.p) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+  for (int64_t e = lo + threadIdx.x; e < hi; e += AR_THREADS) {
+    float s = 0.f;
+    if (ok) {
+      for (int q = 0; q < a.world; ++q)
+        s += __hip_atomic_load(a.slot[q] + par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      s = a.grad[e] * (float)a.world;  // timed out: local gradient (err reports it)
+    }
+    const float g = s * inv_w;
+    if (a.grad_out) a.grad_out[e] = g;
+    if (a.p) {
+      float p = a.p[e], m = a.m[e], v = a.v[e];
+      adam_elem(p, m, v, g, c);
+      a.p[e] = p;
+      a.m[e] = m;
+      a.v[e] = v;
+    }
+  }
+  if (a.p && a.state && b == 0 && threadIdx.x == 0) a.state->step_done = t;
+}
+
+}  // namespace tt

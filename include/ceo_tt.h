@@ -246,6 +246,39 @@ int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n
                             const float* row_loss, const float* grad_loss, float* df, float* dc,
                             tt_stream_t stream);
 
+/* ---- data-parallel gradient exchange over peer memory (xGMI) ------------
+ * Replaces the DistributedDataParallel gradient all-reduce + optim.Adam.step
+ * of a data-parallel training step (training.py:54-55 under DDP)
+ * with ONE launch: every rank publishes its flat gradient into its exchange
+ * region (uncached device memory shared through IPC handles), signals every
+ * peer, waits (bounded) for theirs, sums all ranks' gradients in rank order
+ * (every rank computes bitwise the same mean) and applies Adam.  Setup entry
+ * points allocate / map memory (unlike the compute entries); the caller
+ * exchanges the TT_AR_HANDLE_BYTES handles between ranks (e.g. an all-gather)
+ * and passes every rank's mapped region in tt_ar_peers.  A wait that exceeds
+ * its bound increments *err instead of hanging (the result is then the local
+ * gradient); the caller checks err and falls back to its collective.      */
+#define TT_AR_MAX_RANKS 16
+#define TT_AR_HANDLE_BYTES 64
+typedef struct tt_ar_peers {
+  void* region[TT_AR_MAX_RANKS];   /* every rank's region, mapped in this process */
+} tt_ar_peers;
+int64_t tt_ar_region_bytes(int64_t n);
+int32_t tt_ar_alloc(int64_t bytes, void** region, void* ipc_handle);
+int32_t tt_ar_open(const void* ipc_handle, void** region);
+int32_t tt_ar_close(void* region);
+int32_t tt_ar_free(void* region);
+/* zero the region's flags and slots (all ranks, then a host barrier) */
+int32_t tt_ar_reset(void* region, int64_t n, tt_stream_t stream);
+/* grad_out (nullable, may alias grad) = mean over ranks; params/exp_avg/
+ * exp_avg_sq (nullable params: no Adam) updated with hp at step t =
+ * state->step_cur (state non-NULL) or step_host, which is also the epoch the
+ * flags carry (strictly increasing per region).                             */
+int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t world, int64_t n,
+                             const float* grad, float* grad_out, float* params, float* exp_avg,
+                             float* exp_avg_sq, const tt_adam_hp* hp, tt_state* state,
+                             int64_t step_host, int32_t* err, tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

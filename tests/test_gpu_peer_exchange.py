@@ -1,0 +1,136 @@
+"""Data-parallel gradient exchange over peer memory (tt_ar_*, distributed.
+PeerExchange): ranks are processes sharing the one GPU of the test box (the
+IPC mapping and the flag protocol are the same as across xGMI; the fabric is
+not).  Checked: the mean equals the reference sum / world and is bitwise the
+same on every rank, the fused Adam equals torch's, both gradient slots (step
+parity) and epochs > 2 work, and a full data-parallel FusedTrainer step on
+the exchange matches the reference's DDP step (tests/golden/ddp.npz)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import excluded_param, load_golden, meta_of, normwise, sub
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(fn, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=fn, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    return sorted(res)
+
+
+def _exchange_rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching import _native as N
+        from ceo_firm_matching.distributed import PeerExchange
+        dev = torch.device("cuda:0")
+        n = 21313
+        ex = PeerExchange.create(n, dist.group.WORLD, dev, mode="1")
+        assert ex is not None, "peer exchange could not be set up"
+        hp = N.adam_hp(4e-4)
+        p = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(7))  # same on all ranks
+        m = torch.zeros(n, device=dev)
+        v = torch.zeros(n, device=dev)
+        pr, mr, vr = p.double().cpu(), torch.zeros(n, dtype=torch.float64), torch.zeros(n, dtype=torch.float64)
+        worst, outs = 0.0, []
+        for step in range(1, 7):
+            gens = [torch.Generator().manual_seed(100 * step + r) for r in range(world)]
+            xs = [torch.randn(n, generator=gg) for gg in gens]
+            x = xs[rank].to(dev)
+            out = torch.empty_like(x)
+            ex.run(x, grad_out=out, params=p, exp_avg=m, exp_avg_sq=v, hp=hp, step_host=step)
+            torch.cuda.synchronize()
+            assert int(ex.err.item()) == 0
+            ref = sum(t.double() for t in xs) / world
+            worst = max(worst, float((out.cpu().double() - ref).abs().max() / ref.abs().max()))
+            outs.append(out.cpu().numpy().copy())
+            # torch Adam (fp64) on the reference mean
+            mr = 0.9 * mr + 0.1 * ref
+            vr = 0.999 * vr + 0.001 * ref * ref
+            bc1, bc2 = 1 - 0.9 ** step, 1 - 0.999 ** step
+            pr = pr - (4e-4 / bc1) * mr / ((vr.sqrt() / bc2 ** 0.5) + 1e-8)
+        adam_err = float((p.cpu().double() - pr).abs().max() / pr.abs().max())
+        allo = [None] * world
+        dist.all_gather_object(allo, [o.tobytes() for o in outs])
+        same = all(a == allo[0] for a in allo)
+        q.put((rank, worst, adam_err, same))
+        ex.close()
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, float("inf"), float("inf"), repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_exchange_mean_and_adam(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    for rank, worst, adam_err, same in _spawn(_exchange_rank, world):
+        assert same is True, (rank, same)  # bitwise the same mean on every rank
+        assert worst < 1e-6, (rank, worst)
+        assert adam_err < 1e-5, (rank, adam_err)
+
+
+def _ddp_peer_rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CEO_TT_PEER_AR="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching import CEOFirmMatcher, Config
+        from ceo_firm_matching.engine import FusedTrainer
+        dev = torch.device("cuda:0")
+        g = load_golden("ddp")
+        meta = meta_of(load_golden("cfg2"))
+        cfg = Config()
+        cfg.LATENT_DIM = 64
+        cfg.DROPOUT_P = 0.0
+        cfg.DEVICE = dev
+        m = CEOFirmMatcher(meta, cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()})
+        m = m.to(dev)
+        tr = FusedTrainer(m, lr=cfg.LEARNING_RATE, max_batch=64, seed=0, process_group=dist.group.WORLD)
+        assert tr.peer is not None
+        shard = {k: torch.from_numpy(v) for k, v in sub(g, f"G{world}/shard{rank}").items()}
+        tr.set_data(shard)
+        tr.step(None, 0, shard["target"].shape[0])
+        tr.pop_loss_sum()
+        ref = sub(g, f"G{world}/after_step")
+        errs = {k: normwise(p.detach().cpu().numpy(), ref[k]) for k, p in m.named_parameters()
+                if not excluded_param(k)}
+        q.put((rank, max(errs.values()), max(errs, key=errs.get)))
+    except Exception as e:
+        q.put((rank, float("inf"), repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_data_parallel_step_on_peer_exchange(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    for rank, err, where in _spawn(_ddp_peer_rank, world):
+        assert err < 1e-5, (rank, err, where)

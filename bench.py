@@ -396,7 +396,7 @@ def main():
     # hipGraph replay of whole steps at every world size: the RCCL all-reduce
     # of the data-parallel step is captured with the kernels (no host work
     # per step); --no-graph launches every step eagerly.
-    use_graph = not args.no_graph and (pg is None or dist.get_backend(pg) == "nccl")
+    use_graph = not args.no_graph and (pg is None or dist.get_backend(pg) == "nccl" or tr.peer is not None)
     step_fn = lambda: tr.step_cycle(rows, B, n_batches)  # noqa: E731
     for _ in range(args.warmup):
         step_fn()

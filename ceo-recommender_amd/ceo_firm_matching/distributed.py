@@ -66,7 +66,8 @@ class PeerExchange:
     over ``group``), checks the exchange against ``all_reduce`` on random
     gradients, times both, and returns None -- the caller keeps the
     collective -- unless every rank agrees the exchange is correct and faster.
-    ``CEO_TT_PEER_AR=0`` disables it, ``=1`` skips the timing comparison."""
+    ``CEO_TT_PEER_AR=0`` disables it, ``=1`` skips the timing comparison
+    (and the one-rank-per-GPU requirement: tests only)."""
 
     def __init__(self, lib, regions, own, rank, world, n, device):
         self.lib, self.rank, self.world, self.n, self.device = lib, rank, world, n, device
@@ -87,6 +88,14 @@ class PeerExchange:
             return None
         rank = dist.get_rank(group)
         flag_dev = device if dist.get_backend(group) == "nccl" else "cpu"
+        # the exchange assumes one rank per GPU (its waits need every rank's
+        # kernels resident at once); ranks sharing a device are a rehearsal,
+        # where only a pair is known to co-schedule
+        import socket
+        where = [None] * world
+        dist.all_gather_object(where, (socket.gethostname(), torch.device(device).index or 0), group=group)
+        if len(set(where)) < world and world > 2 and mode != "1":
+            return None
         ok = torch.ones(1, dtype=torch.int32, device=flag_dev)
         ex = None
         try:

@@ -1062,7 +1062,7 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
   a.state = state;
   a.step_host = step_host;
   a.err = err;
-  a.spin_limit = 1u << 26;  // ~4 s of s_sleep(2) polling, then give up (err)
+  a.wait_ticks = 200000000ull;  // 2 s of polling, then give up (err)
   hipLaunchKernelGGL(k_ar_adam, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
   return launch_check();
 }

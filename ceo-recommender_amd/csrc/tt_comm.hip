@@ -41,7 +41,7 @@ struct ArArgs {
   tt_state* state;
   int64_t step_host;
   int32_t* err;                          // set when a wait times out
-  uint32_t spin_limit;
+  uint64_t wait_ticks;                   // wait bound in s_memrealtime ticks (100 MHz)
 };
 
 __device__ __forceinline__ uint64_t ld_flag(const uint64_t* f) {
@@ -73,9 +73,9 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
   __syncthreads();
   if (threadIdx.x < a.world) {
     const uint64_t* f = a.flags[a.rank] + (int64_t)threadIdx.x * a.blocks + b;
-    uint32_t k = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz, chip-wide
     while (ld_flag(f) < epoch) {
-      if (++k > a.spin_limit) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_ticks) {
         ok_s = 0;
         atomicAdd(a.err, 1);
         break;

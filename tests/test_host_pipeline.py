@@ -115,3 +115,12 @@ def test_cli_synthetic_runs(tmp_path):
     assert "Epoch 0: Avg Train Loss = " in r.stdout
     sd = torch.load(str(out), weights_only=True)
     assert "logit_scale" in sd and sd["firm_tower.0.weight"].shape == (64, 204)
+
+
+def test_peer_exchange_not_used_without_a_group():
+    """PeerExchange.create keeps the collective (returns None) for a single
+    process, when disabled, or with no process group initialised -- no HIP
+    call is made on these paths."""
+    from ceo_firm_matching.distributed import PeerExchange
+    assert PeerExchange.create(100, None, "cpu") is None
+    assert PeerExchange.create(100, None, "cpu", mode="0") is None

@@ -564,8 +564,14 @@ __device__ __forceinline__ float tower_x(const TowerDev& T, int64_t drow, int co
 // gradient reduction / Adam arguments (tt_optim.hip)
 // ---------------------------------------------------------------------------
 constexpr int MAX_SEG = 48;
-constexpr int RED_E = 32;   // elements per block
-constexpr int RED_G = 8;    // slab groups per element
+#ifndef TT_RED_E
+#define TT_RED_E 32
+#endif
+#ifndef TT_RED_G
+#define TT_RED_G 16  // 512 threads, 16 slab loads each (A/B over 4x4..64x16 shapes, tools/gpu_bench_multi.sh)
+#endif
+constexpr int RED_E = TT_RED_E;   // elements per block
+constexpr int RED_G = TT_RED_G;   // slab groups per element
 
 struct Seg {
   int64_t off, len;      // range in the parameter arena

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
     const Seg& S = a.seg[si];
     if (S.kind == 0) {
       // fixed summation order (deterministic); UNR independent loads in flight
-      constexpr int UNR = 32;  // 256 slabs / RED_G groups: every load of a thread in flight at once
+      constexpr int UNR = 256 / RED_G;  // 256 slabs / RED_G groups: every load of a thread in flight at once
       const float* base = a.slab[S.tower] + S.slab_off + (e - S.off);
       const int n = S.n_slabs;
       for (int p0 = pg; p0 < n; p0 += RED_G * UNR) {

@@ -208,3 +208,50 @@ def test_contrastive_cpu_path_matches_oracle():
     ce = torch.from_numpy(g["ret/ceo_emb"])
     got = metrics_from_ranks(retrieval_ranks(fe, ce))
     assert got == OC.retrieval_metrics(OC.retrieval_ranks(fe, ce))
+
+
+def test_embedding_mining_exchange_host_argument_errors():
+    """tt_embed_*, tt_triplet_*, tt_ar_*: argument errors decided on the host,
+    before any HIP call (fake host pointers stand in for device memory)."""
+    L = N.lib()
+    m = _model("meta_test")
+    desc = m.tt_desc()
+    b, keep = _batch(desc, 64)
+    buf = _fake()
+    p = buf.ctypes.data
+    ws_ok = N.workspace_bytes(desc, 64)
+    # embeddings: missing output / upstream gradient, short workspace, B = 1 in train mode
+    assert L.tt_embed_forward(ctypes.byref(desc), p, p, p, ctypes.byref(b), 1, 0, 1, p, ws_ok, None, None) \
+        == N.TT_ERR_ARG
+    assert L.tt_embed_forward(ctypes.byref(desc), p, p, p, ctypes.byref(b), 1, 0, 1, p, ws_ok - 4, p, None) \
+        == N.TT_ERR_WORKSPACE
+    b1, keep1 = _batch(desc, 1)
+    assert L.tt_embed_forward(ctypes.byref(desc), p, p, p, ctypes.byref(b1), 1, 0, 1, p, ws_ok, p, None) \
+        == N.TT_ERR_BATCH_TOO_SMALL
+    assert L.tt_embed_backward(ctypes.byref(desc), p, ctypes.byref(b), None, 0, 1, p, ws_ok, p, None) == N.TT_ERR_ARG
+    # semi-hard mining: sizes, d % 4, batch < 2, short workspace, null outputs
+    assert L.tt_triplet_workspace_bytes(0, 10, 16) == N.TT_ERR_ARG
+    assert L.tt_triplet_workspace_bytes(10, 10, 30) == N.TT_ERR_ARG
+    tw = L.tt_triplet_workspace_bytes(100, 100, 32)
+    assert tw > 0
+    assert L.tt_triplet_forward(p, p, 100, 100, 32, 0, ctypes.c_float(0.2), 1, p, tw, p, p, p, None) == N.TT_ERR_ARG
+    assert L.tt_triplet_forward(p, p, 100, 100, 32, 0, ctypes.c_float(0.2), 100, p, tw - 4, p, p, p, None) \
+        == N.TT_ERR_WORKSPACE
+    assert L.tt_triplet_forward(p, p, 100, 100, 32, 0, ctypes.c_float(0.2), 100, p, tw, None, p, p, None) \
+        == N.TT_ERR_ARG
+    assert L.tt_triplet_backward(p, p, 100, 100, 32, 0, 100, p, p, None, p, p, None) == N.TT_ERR_ARG
+    # peer exchange: sizes, rank / world, missing error word, Adam without state
+    assert L.tt_ar_region_bytes(0) == N.TT_ERR_ARG
+    assert L.tt_ar_region_bytes(21313) >= 2 * 21313 * 4
+    peers = N.TTArPeers()
+    for q in range(2):
+        peers.region[q] = p
+    hp = N.adam_hp(4e-4)
+    run = lambda rank, world, n, err, params=None, step=1: L.tt_ar_allreduce_adam(  # noqa: E731
+        ctypes.byref(peers), rank, world, n, p, p, params, p, p, ctypes.byref(hp), None, step, err, None)
+    assert run(0, 0, 100, p) == N.TT_ERR_ARG
+    assert run(2, 2, 100, p) == N.TT_ERR_ARG
+    assert run(0, N.TT_AR_MAX_RANKS + 1, 100, p) == N.TT_ERR_ARG
+    assert run(0, 2, 100, None) == N.TT_ERR_ARG
+    assert run(0, 3, 100, p) == N.TT_ERR_ARG          # region of rank 2 missing
+    assert run(0, 2, 100, p, step=0) == N.TT_ERR_ARG  # no device state: host epochs start at 1

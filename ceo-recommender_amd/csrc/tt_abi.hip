@@ -174,7 +174,11 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   if (kpm > MAX_KP) return TT_ERR_UNSUPPORTED;
   const bool emb = d->n_cat[0] > 0 || d->n_cat[1] > 0;
   // 128-row k_top tiles once the grid still covers every CU twice over
+#ifdef TT_TOP_ROWS
+  P->top_rows = TT_TOP_ROWS;
+#else
   P->top_rows = B >= 16384 ? 128 : 64;
+#endif
   // the 64-row kernels cover the padded rows, so every workspace row that any
   // kernel reads was written earlier in the same step
   P->n_tiles = (int)(padded_rows(B) / ROWS);

@@ -347,6 +347,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / cosine legs")
     ap.add_argument("--no-contrastive", action="store_true", help="skip the cfg-5 contrastive leg")
+    ap.add_argument("--no-side-config", action="store_true",
+                    help="skip the other single-GPU config (PMC passes: counters of the headline config only)")
     ap.add_argument("--dp", action="store_true",
                     help="data-parallel step (all-reduce + Adam) even at world size 1 (tests the N>1 path)")
     args = ap.parse_args()
@@ -519,7 +521,7 @@ def main():
         result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)
         if rank == 0:
             result["cosine_roofline"] = cosine_roofline(dev, D=D)
-        if world == 1:  # the other single-GPU BASELINE config (cfg 2), beside the headline one
+        if world == 1 and not args.no_side_config:  # the other single-GPU BASELINE config (cfg 2)
             others = [c for c in CONFIGS if c != args.config]
             result["other_configs"] = {c: side_config_leg(dev, c) for c in others}
         # drop the training state before the 40 GB (N=1) similarity workspace

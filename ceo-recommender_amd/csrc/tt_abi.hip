@@ -706,7 +706,7 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // split-K so a grad GEMM launches >= ~4 blocks per CU; each split >= 8 K chunks
 static void pick_split(int64_t out_rows, int64_t d, int64_t K, int64_t* split, int64_t* kps) {
-  const int64_t blocks = ((out_rows + BM - 1) / BM) * ((d + BN - 1) / BN);
+  const int64_t blocks = ((out_rows + BlkGrad::BM - 1) / BlkGrad::BM) * ((d + BN - 1) / BN);
   int64_t s = std::max<int64_t>(1, (1024 + blocks - 1) / blocks);
   const int64_t chunks = (K + BK - 1) / BK;
   s = std::min<int64_t>(s, std::max<int64_t>(1, chunks / 8));
@@ -722,10 +722,10 @@ static NceLayout nce_layout(int64_t m, int64_t n, int d) {
   L.n_pad = rup(std::max<int64_t>(n, 1), 16);
   L.nti = L.m_pad / 16;
   L.ntj = L.n_pad / 16;
-  L.n_bm = (m + BM - 1) / BM;
+  L.n_bm = (m + BlkSim::BM - 1) / BlkSim::BM;
   L.n_bn = (n + BN - 1) / BN;
   L.n_rp = L.n_bn * NWN;
-  L.n_cp = L.n_bm * NWM;
+  L.n_cp = L.n_bm * BlkSim::NWM;
   L.d_pad = rup(d, 16);
   L.pntj = L.d_pad / 16;
   pick_split(m, d, L.n_pad, &L.split_f, &L.kps_f);
@@ -754,10 +754,11 @@ static bool nce_args_ok(const float* f, const float* c, int64_t m, int64_t n, in
 static std::once_flag g_nce_attr;
 static void nce_attrs() {
   std::call_once(g_nce_attr, [] {
-    const void* ks[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>, (const void*)k_nce_sim<2>,
-                        (const void*)k_nce_dgrad<SRC_E_ROWS>, (const void*)k_nce_dgrad<SRC_E_AS_MK>};
-    for (const void* k : ks)
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
+    const void* sim[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>, (const void*)k_nce_sim<2>};
+    const void* grad[] = {(const void*)k_nce_dgrad<SRC_E_ROWS>, (const void*)k_nce_dgrad<SRC_E_AS_MK>};
+    for (const void* k : sim) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_SIM);
+    for (const void* k : grad)
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_GRAD);
   });
 }
 
@@ -818,7 +819,7 @@ int32_t tt_nce_forward(const float* f, const float* c, int64_t m, int64_t n, int
   g.colpart = w + L.colpart;
   g.m_pad = L.m_pad;
   g.n_pad = L.n_pad;
-  hipLaunchKernelGGL(k_nce_sim<0>, dim3((unsigned)(L.n_bm * L.n_bn)), dim3(NTH), LDS_BYTES, s, g);
+  hipLaunchKernelGGL(k_nce_sim<0>, dim3((unsigned)(L.n_bm * L.n_bn)), dim3(BlkSim::NTH), LDS_SIM, s, g);
   const int64_t tot = L.m_pad + L.n_pad;
   const int nb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
   hipLaunchKernelGGL(k_nce_sums, dim3(nb), dim3(256), 0, s, w + L.rowpart, L.n_rp, L.m_pad, w + L.colpart, L.n_cp,
@@ -871,8 +872,8 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.part = w + L.part;
     g.p_nti = L.nti;
     g.p_ntj = L.pntj;
-    const dim3 grid((unsigned)(((m + BM - 1) / BM) * g.n_blocks_n), (unsigned)L.split_f);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_ROWS>, grid, dim3(NTH), LDS_BYTES, s, g);
+    const dim3 grid((unsigned)(((m + BlkGrad::BM - 1) / BlkGrad::BM) * g.n_blocks_n), (unsigned)L.split_f);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_ROWS>, grid, dim3(BlkGrad::NTH), LDS_GRAD, s, g);
     const int64_t el = L.nti * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_f, L.nti, L.pntj, m, d, scale, corr, c, n, row0, df);
@@ -890,8 +891,8 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.part = w + L.part;
     g.p_nti = L.ntj;
     g.p_ntj = L.pntj;
-    const dim3 grid((unsigned)(((n + BM - 1) / BM) * g.n_blocks_n), (unsigned)L.split_c);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(NTH), LDS_BYTES, s, g);
+    const dim3 grid((unsigned)(((n + BlkGrad::BM - 1) / BlkGrad::BM) * g.n_blocks_n), (unsigned)L.split_c);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(BlkGrad::NTH), LDS_GRAD, s, g);
     const int64_t el = L.ntj * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_c, L.ntj, L.pntj, n, d, scale, corr, f, m, -row0, dc);
@@ -920,8 +921,8 @@ int32_t tt_retrieval_ranks(const float* f, const float* c, int64_t m, int64_t n,
   GemmArgs g = sim_args(f, c, m, n, d, row0);
   g.diag = diag;
   g.rank_cnt = cnt;
-  const int64_t nblk = ((m + BM - 1) / BM) * g.n_blocks_n;
-  hipLaunchKernelGGL(k_nce_sim<1>, dim3((unsigned)nblk), dim3(NTH), LDS_BYTES, s, g);
+  const int64_t nblk = ((m + BlkSim::BM - 1) / BlkSim::BM) * g.n_blocks_n;
+  hipLaunchKernelGGL(k_nce_sim<1>, dim3((unsigned)nblk), dim3(BlkSim::NTH), LDS_SIM, s, g);
   hipLaunchKernelGGL(k_rank_finish, dim3((unsigned)std::min<int64_t>((m + 255) / 256, 4096)), dim3(256), 0, s, cnt,
                      m, ranks);
   return launch_check();
@@ -962,8 +963,8 @@ int32_t tt_triplet_forward(const float* f, const float* c, int64_t m, int64_t n,
   g.semi_part = semi;
   g.all_part = all;
   g.m_pad = mp;
-  const int64_t nblk = ((m + BM - 1) / BM) * g.n_blocks_n;
-  hipLaunchKernelGGL(k_nce_sim<2>, dim3((unsigned)nblk), dim3(NTH), LDS_BYTES, s, g);
+  const int64_t nblk = ((m + BlkSim::BM - 1) / BlkSim::BM) * g.n_blocks_n;
+  hipLaunchKernelGGL(k_nce_sim<2>, dim3((unsigned)nblk), dim3(BlkSim::NTH), LDS_SIM, s, g);
   hipLaunchKernelGGL(k_triplet_finish, dim3((unsigned)std::min<int64_t>((m + 255) / 256, 4096)), dim3(256), 0, s,
                      semi, all, nrp, mp, m, diag, margin, (float)(1.0 / (double)batch), hardest, row_loss, loss);
   return launch_check();

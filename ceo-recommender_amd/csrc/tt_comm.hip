@@ -60,12 +60,18 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
   // stores performed before the barrier that precedes the flags
   for (int64_t e = lo + threadIdx.x; e < hi; e += AR_THREADS)
     __hip_atomic_store(mine + e, a.grad[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // explicit wait after the release: ROCm 7.2 may drop the s_waitcnt that
+  // follows the fence's write-back when it believes the counter is already
+  // empty (MI355X_MICROARCH.md, compiler hazard) -- the asm is opaque to that
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // 2. signal every rank (one lane per destination)
+  // 2. signal every rank (one lane per destination), behind every wave's wait
   if (threadIdx.x < a.world) {
     uint64_t* f = a.flags[threadIdx.x] + (int64_t)a.rank * a.blocks + b;
-    __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 3. wait for every rank's slice b (bounded)
   __shared__ int ok_s;

@@ -25,10 +25,26 @@
 namespace tt {
 namespace nce {
 
-constexpr int BM = 256, BN = 256, BK = 32, WM = 64, WN = 128;
-constexpr int NWM = BM / WM, NWN = BN / WN, NW = NWM * NWN;  // 4 x 2 = 8 waves
-constexpr int NTH = NW * 64;                                 // 512
+constexpr int BN = 256, BK = 32, WM = 64, WN = 128;
+constexpr int NWN = BN / WN;                                 // 2 waves along N
 constexpr int TM = WM / 16, TN = WN / 16;                    // 4 x 8 MFMA tiles / wave
+// Block shapes (rows BM x BN columns, 8 waves of WM x WN, one block per CU):
+// 256 x 256.  The similarity kernels' BM is a build knob (TT_NCE_SIM_BM=128:
+// 4 waves, 72 KB of LDS, two blocks per CU so one block's staging runs beside
+// the other's MFMAs).  Measured at N = 100k, D = 256 (tools/gpu_nce_ab.sh):
+// 128 rows 31.9 ms fwd / 28.2 ms ranks vs 256 rows 29.6 / 25.1 -- the 128-row
+// block needs 48 staging VGPRs per lane (12 float4 instead of 8) and spills
+// at the 256-register limit of two waves per SIMD.  Every wave keeps its
+// 64 x 128 tile and reduction order, so results are bitwise the same.
+#ifndef TT_NCE_SIM_BM
+#define TT_NCE_SIM_BM 256
+#endif
+template <int BM_> struct Blk {
+  static constexpr int BM = BM_, NWM = BM_ / WM, NW = NWM * NWN, NTH = NW * 64;
+  static constexpr int MIN_WAVES = BM_ == 128 ? 2 : 1;  // waves per SIMD (blocks per CU x NW / 4)
+};
+using BlkSim = Blk<TT_NCE_SIM_BM>;
+using BlkGrad = Blk<256>;
 constexpr int TILE = 256;                                    // floats per 16x16 tile
 constexpr float SUM_MIN = 1e-30f;  // row/col sums below this: exp underflow (reported)
 
@@ -51,18 +67,23 @@ constexpr int NPL = 3;                // planes h, m, l
 //    LDS table) -- conflict-free reads and row-contiguous staging writes;
 //  * padded (the gradient kernels, whose k-major staging writes 16 rows at one
 //    k): 80-B rows.
-template <bool SWZ> struct Lay {
+template <bool SWZ, int ROWS> struct Lay {
   static constexpr int LDK = SWZ ? BK : BK + 8;  // bf16 per LDS row
-  static constexpr int PLANE = BM * LDK;         // bf16 per plane of one operand (BM == BN)
+  static constexpr int PLANE = ROWS * LDK;       // bf16 per plane of one operand
   static constexpr int OPND = NPL * PLANE;       // bf16 per operand
 };
 __device__ __forceinline__ int lds_swz(int m) { return (0x78 >> (2 * ((m >> 2) & 3))) & 3; }
 template <bool SWZ>
 __device__ __forceinline__ int lds_off(int m, int k) {  // bf16 offset of (m, k) in a plane
-  if constexpr (SWZ) return m * Lay<SWZ>::LDK + ((((k >> 3) ^ lds_swz(m)) << 3) | (k & 7));
-  else return m * Lay<SWZ>::LDK + k;
+  if constexpr (SWZ) return m * Lay<SWZ, 1>::LDK + ((((k >> 3) ^ lds_swz(m)) << 3) | (k & 7));
+  else return m * Lay<SWZ, 1>::LDK + k;
 }
-constexpr size_t LDS_BYTES = sizeof(uint16_t) * 2 * Lay<false>::OPND;  // A + B, single buffer (120 KB max)
+// A (BM rows) + B (BN rows), single stage
+template <int BM_, bool SWZ>
+constexpr size_t lds_bytes() { return sizeof(uint16_t) * (Lay<SWZ, BM_>::OPND + Lay<SWZ, BN>::OPND); }
+constexpr size_t LDS_SIM = lds_bytes<BlkSim::BM, true>();     // 96 KB (72 KB at BM 128); both operands SRC_MK
+constexpr size_t LDS_GRAD = lds_bytes<BlkGrad::BM, false>();  // 120 KB
+static_assert(BlkSim::MIN_WAVES == 1 || 2 * LDS_SIM <= 160 * 1024, "two similarity blocks per CU");
 
 
 // Where an operand comes from.  LDS always holds [m][k] bf16 planes.
@@ -153,23 +174,25 @@ __device__ __forceinline__ uint64_t row_min16(uint64_t v) {
 }
 
 // ---- global -> registers (4 float4 per thread per operand per K chunk) ----
-template <int S>
-__device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0, float4 (&v)[4]) {
-  if constexpr (S == SRC_MK) {  // tile BM x BK from G[m][k]: 8 float4 per row
+// (ROWS x BK floats per operand tile, NT threads: ROWS * 8 / NT float4 each)
+template <int S, int ROWS, int NT>
+__device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0, float4 (&v)[ROWS * 8 / NT]) {
+  constexpr int NQ = ROWS * 8 / NT;
+  if constexpr (S == SRC_MK) {  // tile ROWS x BK from G[m][k]: 8 float4 per row
     const auto rs = buf_rsrc(o.p + m0 * o.ld, (o.mdim - m0) * o.ld * 4);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = (int)threadIdx.x + q * NTH;
+    for (int q = 0; q < NQ; ++q) {
+      const int e = (int)threadIdx.x + q * NT;
       const int r = e >> 3, kq = (e & 7) * 4;
       const bool ok = k0 + kq < o.kdim;
       v[q] = buf_f32x4(rs, ok ? (uint32_t)((r * o.ld + k0 + kq) * 4) : BUF_OOB);
     }
-  } else if constexpr (S == SRC_KROWS) {  // G[k][m]: 256 m (lanes) x 8 k-quads, 4 scalar loads
+  } else if constexpr (S == SRC_KROWS) {  // G[k][m]: ROWS m (lanes) x 8 k-quads, 4 scalar loads
     const auto rs = buf_rsrc(o.p + k0 * o.ld, (o.kdim - k0) * o.ld * 4);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = (int)threadIdx.x + q * NTH;
-      const int ml = e & 255, kq = (e >> 8) * 4;
+    for (int q = 0; q < NQ; ++q) {
+      const int e = (int)threadIdx.x + q * NT;
+      const int ml = e % ROWS, kq = (e / ROWS) * 4;
       const bool ok = m0 + ml < o.mdim;
       float x[4];
 #pragma unroll
@@ -177,14 +200,14 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
         x[c] = buf_f32(rs, ok ? (uint32_t)(((kq + c) * o.ld + m0 + ml) * 4) : BUF_OOB);
       v[q] = make_float4(x[0], x[1], x[2], x[3]);
     }
-  } else if constexpr (S == SRC_E_ROWS) {  // E'(i, j..j+3): 256 i x 8 j-quads
+  } else if constexpr (S == SRC_E_ROWS) {  // E'(i, j..j+3): ROWS i x 8 j-quads
     const int64_t ti0 = m0 >> 4, tj0 = k0 >> 4;
     const int64_t tiles = (o.nti - ti0) * o.ntj - tj0;  // tiles from (ti0, tj0) to the end of E
     const auto rs = buf_rsrc(o.p + (ti0 * o.ntj + tj0) * TILE, tiles * TILE * 4);
     const auto ra = buf_rsrc(o.a, o.nti * 16 * 4), rb = buf_rsrc(o.b, o.ntj * 16 * 4);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = (int)threadIdx.x + q * NTH;
+    for (int q = 0; q < NQ; ++q) {
+      const int e = (int)threadIdx.x + q * NT;
       const int il = e >> 3, jq = (e & 7) * 4;
       const int64_t gi = m0 + il, gj = k0 + jq;
       const bool ok = (gj >> 4) < o.ntj && (gi >> 4) < o.nti;
@@ -198,14 +221,14 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
       for (int c = 0; c < 4; ++c) x[c] = buf_f32(rs, ok ? (base + 4 * c) * 4 : BUF_OOB);
       v[q] = make_float4(x[0] * (ai + bj.x), x[1] * (ai + bj.y), x[2] * (ai + bj.z), x[3] * (ai + bj.w));
     }
-  } else if constexpr (S == SRC_E_AS_MK) {  // E tiles as [m = j][k = i]: 16 j-tiles x 2 i-tiles
+  } else if constexpr (S == SRC_E_AS_MK) {  // E tiles as [m = j][k = i]: ROWS/16 j-tiles x 2 i-tiles
     const int64_t tj0 = m0 >> 4, ti0 = k0 >> 4;
     const int64_t tiles = (o.nti - ti0) * o.ntj - tj0;
     const auto rs = buf_rsrc(o.p + (ti0 * o.ntj + tj0) * TILE, tiles * TILE * 4);
     const auto ra = buf_rsrc(o.a, o.nti * 16 * 4), rb = buf_rsrc(o.b, o.ntj * 16 * 4);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = (int)threadIdx.x + q * NTH;
+    for (int q = 0; q < NQ; ++q) {
+      const int e = (int)threadIdx.x + q * NT;
       const int t = e >> 6, ln = e & 63;
       const int tm = t >> 1, tk = t & 1;
       const int64_t tj = tj0 + tm, ti = ti0 + tk;
@@ -219,17 +242,17 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
 }
 
 // split the staged float4s into the three bf16 planes of LDS [m][k]
-template <int S, bool SWZ>
-__device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[4]) {
-  constexpr int PLANE = Lay<SWZ>::PLANE;
+template <int S, bool SWZ, int ROWS, int NT>
+__device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[ROWS * 8 / NT]) {
+  constexpr int PLANE = Lay<SWZ, ROWS>::PLANE;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = (int)threadIdx.x + q * NTH;
+  for (int q = 0; q < ROWS * 8 / NT; ++q) {
+    const int e = (int)threadIdx.x + q * NT;
     int m, k;  // the thread's float4 holds k .. k+3 of row m
     if constexpr (S == SRC_MK || S == SRC_E_ROWS) {
       m = e >> 3; k = (e & 7) * 4;
     } else if constexpr (S == SRC_KROWS) {
-      m = e & 255; k = (e >> 8) * 4;
+      m = e % ROWS; k = (e / ROWS) * 4;
     } else {  // SRC_E_AS_MK: the tile float4 = 4 consecutive E rows i = k
       const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
       m = 16 * tm + (ln & 15); k = 16 * tk + 4 * (ln >> 4);
@@ -245,51 +268,52 @@ __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[4]) {
 }
 
 // MFMA operand: 8 consecutive k (k = kk + 8g .. +7) of row m, one plane
-template <bool SWZ>
+template <bool SWZ, int ROWS>
 __device__ __forceinline__ bf16x8 frag(const uint16_t* L, int plane, int m, int g) {
-  return *reinterpret_cast<const bf16x8*>(L + plane * Lay<SWZ>::PLANE + lds_off<SWZ>(m, 8 * g));
+  return *reinterpret_cast<const bf16x8*>(L + plane * Lay<SWZ, ROWS>::PLANE + lds_off<SWZ>(m, 8 * g));
 }
 
 
 // Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T.  One LDS
 // stage (120 KB); the next chunk's global loads are in flight during the
 // MFMAs of the current one.
-template <int SA, int SB>
+template <int SA, int SB, int BM_>
 __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
                                           uint16_t* smem, f32x4 (&acc)[TM][TN]) {
+  constexpr int NT = Blk<BM_>::NTH;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   const int wm = w / NWN, wn = w % NWN;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
-  float4 va[4], vb[4];
+  float4 va[BM_ * 8 / NT], vb[BN * 8 / NT];
   const int nch = (int)((ke - kb + BK - 1) / BK);
   if (nch <= 0) return;
   constexpr bool SWZ = SA == SRC_MK && SB == SRC_MK;
   uint16_t* As = smem;
-  uint16_t* Bs = smem + Lay<SWZ>::OPND;
-  load_opnd<SA>(g_.A, m0, kb, va);
-  load_opnd<SB>(g_.B, n0, kb, vb);
+  uint16_t* Bs = smem + Lay<SWZ, BM_>::OPND;
+  load_opnd<SA, BM_, NT>(g_.A, m0, kb, va);
+  load_opnd<SB, BN, NT>(g_.B, n0, kb, vb);
   for (int c = 0; c < nch; ++c) {
     __syncthreads();  // the previous chunk's fragments have been read
-    store_opnd<SA, SWZ>(As, va);
-    store_opnd<SB, SWZ>(Bs, vb);
+    store_opnd<SA, SWZ, BM_, NT>(As, va);
+    store_opnd<SB, SWZ, BN, NT>(Bs, vb);
     __syncthreads();
     if (c + 1 < nch) {
-      load_opnd<SA>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
-      load_opnd<SB>(g_.B, n0, kb + (int64_t)(c + 1) * BK, vb);
+      load_opnd<SA, BM_, NT>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
+      load_opnd<SB, BN, NT>(g_.B, n0, kb + (int64_t)(c + 1) * BK, vb);
     }
     bf16x8 a[TM][NPL];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int p = 0; p < NPL; ++p) a[i][p] = frag<SWZ>(As, p, wm * WM + 16 * i + r, g);
+      for (int p = 0; p < NPL; ++p) a[i][p] = frag<SWZ, BM_>(As, p, wm * WM + 16 * i + r, g);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bf16x8 b[NPL];
 #pragma unroll
-      for (int p = 0; p < NPL; ++p) b[p] = frag<SWZ>(Bs, p, wn * WN + 16 * j + r, g);
+      for (int p = 0; p < NPL; ++p) b[p] = frag<SWZ, BN>(Bs, p, wn * WN + 16 * j + r, g);
 #pragma unroll
       for (int q = 0; q < 6; ++q)
 #pragma unroll
@@ -312,14 +336,15 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t nblk) {
 // k_nce_sim: S = F C^T (MODE 0: InfoNCE exp/partials; MODE 1: rank counts)
 // ---------------------------------------------------------------------------
 template <int MODE>
-__global__ __launch_bounds__(NTH) void k_nce_sim(GemmArgs a) {
+__global__ __launch_bounds__(BlkSim::NTH, BlkSim::MIN_WAVES) void k_nce_sim(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int NWM = BlkSim::NWM;
   const int64_t nblk = (int64_t)gridDim.x;
   const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
   const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
-  const int64_t m0 = bm * BM, n0 = bn * BN;
+  const int64_t m0 = bm * BlkSim::BM, n0 = bn * BN;
   f32x4 acc[TM][TN];
-  gemm_loop<SRC_MK, SRC_MK>(a, m0, n0, 0, a.A.kdim, smem, acc);
+  gemm_loop<SRC_MK, SRC_MK, BlkSim::BM>(a, m0, n0, 0, a.A.kdim, smem, acc);
 
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   const int wm = w / NWN, wn = w % NWN;
@@ -474,17 +499,17 @@ __global__ __launch_bounds__(256) void k_nce_diag(const float* __restrict__ F, c
 // accumulator-layout tiles part[split][ti][tj][256]
 // ---------------------------------------------------------------------------
 template <int SA>
-__global__ __launch_bounds__(NTH) void k_nce_dgrad(GemmArgs a) {
+__global__ __launch_bounds__(BlkGrad::NTH) void k_nce_dgrad(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int64_t nblk = (int64_t)gridDim.x;
   const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
   const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
-  const int64_t m0 = bm * BM, n0 = bn * BN;
+  const int64_t m0 = bm * BlkGrad::BM, n0 = bn * BN;
   const int64_t split = blockIdx.y;
   const int64_t kb = split * a.k_per_split;
   const int64_t ke = min(kb + a.k_per_split, a.A.kdim);
   f32x4 acc[TM][TN];
-  gemm_loop<SA, SRC_KROWS>(a, m0, n0, kb, ke, smem, acc);
+  gemm_loop<SA, SRC_KROWS, BlkGrad::BM>(a, m0, n0, kb, ke, smem, acc);
   const int w = wave_id(), l = lane_id();
   const int wm = w / NWN, wn = w % NWN;
 #pragma unroll

@@ -88,11 +88,11 @@ static_assert(BlkSim::MIN_WAVES == 1 || 2 * LDS_SIM <= 160 * 1024, "two similari
 
 // Where an operand comes from.  LDS always holds [m][k] bf16 planes.
 enum Src : int {
-  // every source hands a thread 4 consecutive k, so the split planes are
-  // written along k (8-byte LDS writes, no transposition)
+  // every source hands a thread 4 (SRC_KROWS: 8) consecutive k, so the split
+  // planes are written along k (8- / 16-byte LDS writes, no transposition)
   SRC_MK = 0,       // row-major G[m][k] (ld): one float4 along k
   SRC_E_AS_MK = 3,  // E tiles, m = E col j, k = E row i: the tile's float4 (4 rows i)  (dC = E'^T F)
-  SRC_KROWS = 4,    // row-major G[k][m] (ld): 4 scalar loads down k, lanes along m (coalesced)
+  SRC_KROWS = 4,    // row-major G[k][m] (ld): 8 scalar loads down k, lanes along m (coalesced)
   SRC_E_ROWS = 5,   // E tiles, m = E row i, k = E col j: 4 scalar loads along j     (dF = E' C)
 };
 
@@ -187,18 +187,20 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
       const bool ok = k0 + kq < o.kdim;
       v[q] = buf_f32x4(rs, ok ? (uint32_t)((r * o.ld + k0 + kq) * 4) : BUF_OOB);
     }
-  } else if constexpr (S == SRC_KROWS) {  // G[k][m]: ROWS m (lanes) x 8 k-quads, 4 scalar loads
+  } else if constexpr (S == SRC_KROWS) {  // G[k][m]: ROWS m (lanes) x 4 k-octets, 8 scalar loads
+    // (an item is 8 consecutive k = one 16-B LDS granule per plane, v[2t] | v[2t + 1])
     const auto rs = buf_rsrc(o.p + k0 * o.ld, (o.kdim - k0) * o.ld * 4);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int e = (int)threadIdx.x + q * NT;
-      const int ml = e % ROWS, kq = (e / ROWS) * 4;
+    for (int t = 0; t < NQ / 2; ++t) {
+      const int e = (int)threadIdx.x + t * NT;
+      const int ml = e % ROWS, k8 = (e / ROWS) * 8;
       const bool ok = m0 + ml < o.mdim;
-      float x[4];
+      float x[8];
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        x[c] = buf_f32(rs, ok ? (uint32_t)(((kq + c) * o.ld + m0 + ml) * 4) : BUF_OOB);
-      v[q] = make_float4(x[0], x[1], x[2], x[3]);
+      for (int c = 0; c < 8; ++c)
+        x[c] = buf_f32(rs, ok ? (uint32_t)(((k8 + c) * o.ld + m0 + ml) * 4) : BUF_OOB);
+      v[2 * t] = make_float4(x[0], x[1], x[2], x[3]);
+      v[2 * t + 1] = make_float4(x[4], x[5], x[6], x[7]);
     }
   } else if constexpr (S == SRC_E_ROWS) {  // E'(i, j..j+3): ROWS i x 8 j-quads
     const int64_t ti0 = m0 >> 4, tj0 = k0 >> 4;
@@ -245,14 +247,31 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
 template <int S, bool SWZ, int ROWS, int NT>
 __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[ROWS * 8 / NT]) {
   constexpr int PLANE = Lay<SWZ, ROWS>::PLANE;
+  if constexpr (S == SRC_KROWS) {
+    // lanes run along m at one k-octet: 16-B writes of 80-B rows hit 16
+    // distinct 16-B slots per 16 lanes (8-B writes of 4 k would pair rows
+    // m and m + 16 on one bank: 2-way conflicts)
+#pragma unroll
+    for (int t = 0; t < ROWS * 4 / NT; ++t) {
+      const int e = (int)threadIdx.x + t * NT;
+      const int m = e % ROWS, k8 = (e / ROWS) * 8;
+      const float x[8] = {v[2 * t].x,     v[2 * t].y,     v[2 * t].z,     v[2 * t].w,
+                          v[2 * t + 1].x, v[2 * t + 1].y, v[2 * t + 1].z, v[2 * t + 1].w};
+      bf16x8 pl[NPL];
+      split8x3(x, pl);
+      uint16_t* d = L + lds_off<SWZ>(m, k8);
+      *reinterpret_cast<bf16x8*>(d) = pl[0];
+      *reinterpret_cast<bf16x8*>(d + PLANE) = pl[1];
+      *reinterpret_cast<bf16x8*>(d + 2 * PLANE) = pl[2];
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < ROWS * 8 / NT; ++q) {
     const int e = (int)threadIdx.x + q * NT;
     int m, k;  // the thread's float4 holds k .. k+3 of row m
     if constexpr (S == SRC_MK || S == SRC_E_ROWS) {
       m = e >> 3; k = (e & 7) * 4;
-    } else if constexpr (S == SRC_KROWS) {
-      m = e % ROWS; k = (e / ROWS) * 4;
     } else {  // SRC_E_AS_MK: the tile float4 = 4 consecutive E rows i = k
       const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
       m = 16 * tm + (ln & 15); k = 16 * tk + 4 * (ln >> 4);

@@ -93,7 +93,7 @@ enum Src : int {
   SRC_MK = 0,       // row-major G[m][k] (ld): one float4 along k
   SRC_E_AS_MK = 3,  // E tiles, m = E col j, k = E row i: the tile's float4 (4 rows i)  (dC = E'^T F)
   SRC_KROWS = 4,    // row-major G[k][m] (ld): 8 scalar loads down k, lanes along m (coalesced)
-  SRC_E_ROWS = 5,   // E tiles, m = E row i, k = E col j: 4 scalar loads along j     (dF = E' C)
+  SRC_E_ROWS = 5,   // E tiles, m = E row i, k = E col j: the tile float4, quad-transposed (dF = E' C)
 };
 
 // Buffer resources (SGPR base + 32-bit lane offsets; reads outside
@@ -202,7 +202,10 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
       v[2 * t] = make_float4(x[0], x[1], x[2], x[3]);
       v[2 * t + 1] = make_float4(x[4], x[5], x[6], x[7]);
     }
-  } else if constexpr (S == SRC_E_ROWS) {  // E'(i, j..j+3): ROWS i x 8 j-quads
+  } else if constexpr (S == SRC_E_ROWS) {  // E tiles as [m = i][k = j]: ROWS/16 i-tiles x 2 j-tiles
+    // one coalesced float4 per lane (4 rows i at one column j, the MFMA
+    // accumulator layout k_nce_sim stored), quad-transposed in registers to
+    // 4 consecutive j of one row i
     const int64_t ti0 = m0 >> 4, tj0 = k0 >> 4;
     const int64_t tiles = (o.nti - ti0) * o.ntj - tj0;  // tiles from (ti0, tj0) to the end of E
     const auto rs = buf_rsrc(o.p + (ti0 * o.ntj + tj0) * TILE, tiles * TILE * 4);
@@ -210,17 +213,14 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int e = (int)threadIdx.x + q * NT;
-      const int il = e >> 3, jq = (e & 7) * 4;
-      const int64_t gi = m0 + il, gj = k0 + jq;
-      const bool ok = (gj >> 4) < o.ntj && (gi >> 4) < o.nti;
-      // element (ii, jj) of a tile: lane jj + 16 (ii / 4), slot ii % 4
-      const uint32_t base = (uint32_t)(((il >> 4) * o.ntj + (jq >> 4)) * TILE +
-                                       ((gj & 15) + 16 * ((gi & 15) >> 2)) * 4 + (gi & 3));
-      const float ai = buf_f32(ra, ok ? (uint32_t)(gi * 4) : BUF_OOB);
-      const float4 bj = buf_f32x4(rb, ok ? (uint32_t)(gj * 4) : BUF_OOB);
-      float x[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) x[c] = buf_f32(rs, ok ? (base + 4 * c) * 4 : BUF_OOB);
+      const int t = e >> 6, ln = e & 63;
+      const int tm = t >> 1, tk = t & 1;
+      const int64_t ti = ti0 + tm, tj = tj0 + tk;
+      const bool ok = ti < o.nti && tj < o.ntj;
+      const f32x4 x = quad_transpose(__builtin_bit_cast(
+          f32x4, buf_f32x4(rs, ok ? (uint32_t)(((tm * o.ntj + tk) * TILE + ln * 4) * 4) : BUF_OOB)));
+      const float ai = buf_f32(ra, ok ? (uint32_t)((ti * 16 + 4 * (ln >> 4) + (ln & 3)) * 4) : BUF_OOB);
+      const float4 bj = buf_f32x4(rb, ok ? (uint32_t)((tj * 16 + (ln & 12)) * 4) : BUF_OOB);
       v[q] = make_float4(x[0] * (ai + bj.x), x[1] * (ai + bj.y), x[2] * (ai + bj.z), x[3] * (ai + bj.w));
     }
   } else if constexpr (S == SRC_E_AS_MK) {  // E tiles as [m = j][k = i]: ROWS/16 j-tiles x 2 i-tiles
@@ -270,8 +270,11 @@ __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[ROWS *
   for (int q = 0; q < ROWS * 8 / NT; ++q) {
     const int e = (int)threadIdx.x + q * NT;
     int m, k;  // the thread's float4 holds k .. k+3 of row m
-    if constexpr (S == SRC_MK || S == SRC_E_ROWS) {
+    if constexpr (S == SRC_MK) {
       m = e >> 3; k = (e & 7) * 4;
+    } else if constexpr (S == SRC_E_ROWS) {  // quad-transposed tile float4: row i, 4 consecutive j
+      const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
+      m = 16 * tm + 4 * (ln >> 4) + (ln & 3); k = 16 * tk + (ln & 12);
     } else {  // SRC_E_AS_MK: the tile float4 = 4 consecutive E rows i = k
       const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
       m = 16 * tm + (ln & 15); k = 16 * tk + 4 * (ln >> 4);

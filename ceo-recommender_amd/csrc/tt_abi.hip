@@ -706,7 +706,7 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // split-K so a grad GEMM launches >= ~4 blocks per CU; each split >= 8 K chunks
 static void pick_split(int64_t out_rows, int64_t d, int64_t K, int64_t* split, int64_t* kps) {
-  const int64_t blocks = ((out_rows + BlkGrad::BM - 1) / BlkGrad::BM) * ((d + BN - 1) / BN);
+  const int64_t blocks = ((out_rows + CfgGrad::BM - 1) / CfgGrad::BM) * ((d + CfgGrad::BN - 1) / CfgGrad::BN);
   int64_t s = std::max<int64_t>(1, (1024 + blocks - 1) / blocks);
   const int64_t chunks = (K + BK - 1) / BK;
   s = std::min<int64_t>(s, std::max<int64_t>(1, chunks / 8));
@@ -722,10 +722,10 @@ static NceLayout nce_layout(int64_t m, int64_t n, int d) {
   L.n_pad = rup(std::max<int64_t>(n, 1), 16);
   L.nti = L.m_pad / 16;
   L.ntj = L.n_pad / 16;
-  L.n_bm = (m + BlkSim::BM - 1) / BlkSim::BM;
-  L.n_bn = (n + BN - 1) / BN;
-  L.n_rp = L.n_bn * NWN;
-  L.n_cp = L.n_bm * BlkSim::NWM;
+  L.n_bm = (m + CfgSim::BM - 1) / CfgSim::BM;
+  L.n_bn = (n + CfgSim::BN - 1) / CfgSim::BN;
+  L.n_rp = L.n_bn * CfgSim::NWN;
+  L.n_cp = L.n_bm * CfgSim::NWM;
   L.d_pad = rup(d, 16);
   L.pntj = L.d_pad / 16;
   pick_split(m, d, L.n_pad, &L.split_f, &L.kps_f);
@@ -769,7 +769,7 @@ static GemmArgs sim_args(const float* f, const float* c, int64_t m, int64_t n, i
   g.B = Opnd{c, d, n, d, 0, 0, nullptr, nullptr};
   g.M = m;
   g.N = n;
-  g.n_blocks_n = (int)((n + BN - 1) / BN);
+  g.n_blocks_n = (int)((n + CfgSim::BN - 1) / CfgSim::BN);
   g.row0 = row0;
   return g;
 }
@@ -819,7 +819,7 @@ int32_t tt_nce_forward(const float* f, const float* c, int64_t m, int64_t n, int
   g.colpart = w + L.colpart;
   g.m_pad = L.m_pad;
   g.n_pad = L.n_pad;
-  hipLaunchKernelGGL(k_nce_sim<0>, dim3((unsigned)(L.n_bm * L.n_bn)), dim3(BlkSim::NTH), LDS_SIM, s, g);
+  hipLaunchKernelGGL(k_nce_sim<0>, dim3((unsigned)(L.n_bm * L.n_bn)), dim3(CfgSim::NTH), LDS_SIM, s, g);
   const int64_t tot = L.m_pad + L.n_pad;
   const int nb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
   hipLaunchKernelGGL(k_nce_sums, dim3(nb), dim3(256), 0, s, w + L.rowpart, L.n_rp, L.m_pad, w + L.colpart, L.n_cp,
@@ -868,12 +868,12 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.M = m;
     g.N = d;
     g.k_per_split = L.kps_f;
-    g.n_blocks_n = (int)((d + BN - 1) / BN);
+    g.n_blocks_n = (int)((d + CfgGrad::BN - 1) / CfgGrad::BN);
     g.part = w + L.part;
     g.p_nti = L.nti;
     g.p_ntj = L.pntj;
-    const dim3 grid((unsigned)(((m + BlkGrad::BM - 1) / BlkGrad::BM) * g.n_blocks_n), (unsigned)L.split_f);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_ROWS>, grid, dim3(BlkGrad::NTH), LDS_GRAD, s, g);
+    const dim3 grid((unsigned)(((m + CfgGrad::BM - 1) / CfgGrad::BM) * g.n_blocks_n), (unsigned)L.split_f);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_ROWS>, grid, dim3(CfgGrad::NTH), LDS_GRAD, s, g);
     const int64_t el = L.nti * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_f, L.nti, L.pntj, m, d, scale, corr, c, n, row0, df);
@@ -887,12 +887,12 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.M = n;
     g.N = d;
     g.k_per_split = L.kps_c;
-    g.n_blocks_n = (int)((d + BN - 1) / BN);
+    g.n_blocks_n = (int)((d + CfgGrad::BN - 1) / CfgGrad::BN);
     g.part = w + L.part;
     g.p_nti = L.ntj;
     g.p_ntj = L.pntj;
-    const dim3 grid((unsigned)(((n + BlkGrad::BM - 1) / BlkGrad::BM) * g.n_blocks_n), (unsigned)L.split_c);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(BlkGrad::NTH), LDS_GRAD, s, g);
+    const dim3 grid((unsigned)(((n + CfgGrad::BM - 1) / CfgGrad::BM) * g.n_blocks_n), (unsigned)L.split_c);
+    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(CfgGrad::NTH), LDS_GRAD, s, g);
     const int64_t el = L.ntj * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_c, L.ntj, L.pntj, n, d, scale, corr, f, m, -row0, dc);
@@ -921,8 +921,8 @@ int32_t tt_retrieval_ranks(const float* f, const float* c, int64_t m, int64_t n,
   GemmArgs g = sim_args(f, c, m, n, d, row0);
   g.diag = diag;
   g.rank_cnt = cnt;
-  const int64_t nblk = ((m + BlkSim::BM - 1) / BlkSim::BM) * g.n_blocks_n;
-  hipLaunchKernelGGL(k_nce_sim<1>, dim3((unsigned)nblk), dim3(BlkSim::NTH), LDS_SIM, s, g);
+  const int64_t nblk = ((m + CfgSim::BM - 1) / CfgSim::BM) * g.n_blocks_n;
+  hipLaunchKernelGGL(k_nce_sim<1>, dim3((unsigned)nblk), dim3(CfgSim::NTH), LDS_SIM, s, g);
   hipLaunchKernelGGL(k_rank_finish, dim3((unsigned)std::min<int64_t>((m + 255) / 256, 4096)), dim3(256), 0, s, cnt,
                      m, ranks);
   return launch_check();
@@ -932,7 +932,7 @@ int32_t tt_retrieval_ranks(const float* f, const float* c, int64_t m, int64_t n,
 static int64_t triplet_ws_floats(int64_t m, int64_t n, int64_t* m_pad, int64_t* n_rp) {
   using namespace tt::nce;
   *m_pad = (m + 63) / 64 * 64;
-  *n_rp = ((n + BN - 1) / BN) * NWN;
+  *n_rp = ((n + CfgSim::BN - 1) / CfgSim::BN) * CfgSim::NWN;
   return *m_pad + 2 * 2 * (*n_rp) * (*m_pad);  // diag | semi_part (u64) | all_part (u64)
 }
 
@@ -963,8 +963,8 @@ int32_t tt_triplet_forward(const float* f, const float* c, int64_t m, int64_t n,
   g.semi_part = semi;
   g.all_part = all;
   g.m_pad = mp;
-  const int64_t nblk = ((m + BlkSim::BM - 1) / BlkSim::BM) * g.n_blocks_n;
-  hipLaunchKernelGGL(k_nce_sim<2>, dim3((unsigned)nblk), dim3(BlkSim::NTH), LDS_SIM, s, g);
+  const int64_t nblk = ((m + CfgSim::BM - 1) / CfgSim::BM) * g.n_blocks_n;
+  hipLaunchKernelGGL(k_nce_sim<2>, dim3((unsigned)nblk), dim3(CfgSim::NTH), LDS_SIM, s, g);
   hipLaunchKernelGGL(k_triplet_finish, dim3((unsigned)std::min<int64_t>((m + 255) / 256, 4096)), dim3(256), 0, s,
                      semi, all, nrp, mp, m, diag, margin, (float)(1.0 / (double)batch), hardest, row_loss, loss);
   return launch_check();

@@ -25,26 +25,37 @@
 namespace tt {
 namespace nce {
 
-constexpr int BN = 256, BK = 32, WM = 64, WN = 128;
-constexpr int NWN = BN / WN;                                 // 2 waves along N
-constexpr int TM = WM / 16, TN = WN / 16;                    // 4 x 8 MFMA tiles / wave
-// Block shapes (rows BM x BN columns, 8 waves of WM x WN, one block per CU):
-// 256 x 256.  The similarity kernels' BM is a build knob (TT_NCE_SIM_BM=128:
-// 4 waves, 72 KB of LDS, two blocks per CU so one block's staging runs beside
-// the other's MFMAs).  Measured at N = 100k, D = 256 (tools/gpu_nce_ab.sh):
-// 128 rows 31.9 ms fwd / 28.2 ms ranks vs 256 rows 29.6 / 25.1 -- the 128-row
-// block needs 48 staging VGPRs per lane (12 float4 instead of 8) and spills
-// at the 256-register limit of two waves per SIMD.  Every wave keeps its
-// 64 x 128 tile and reduction order, so results are bitwise the same.
-#ifndef TT_NCE_SIM_BM
-#define TT_NCE_SIM_BM 256
-#endif
-template <int BM_> struct Blk {
-  static constexpr int BM = BM_, NWM = BM_ / WM, NW = NWM * NWN, NTH = NW * 64;
-  static constexpr int MIN_WAVES = BM_ == 128 ? 2 : 1;  // waves per SIMD (blocks per CU x NW / 4)
+constexpr int BK = 32, WM = 64, TM = WM / 16;  // K chunk; waves own WM rows = 4 MFMA row tiles
+// Block shapes: BM x BN output tiles, 8 waves of WM x WN (TN = WN / 16 column
+// tiles per wave), one block per CU.
+//  * gradient kernels, Cfg<256, 256, 128>: one 120 KB LDS stage (padded
+//    k-major layout); the next chunk's global loads fly during the MFMAs, its
+//    split and LDS writes wait for the barrier after them;
+//  * similarity kernels: the same (default), or with TT_NCE_SIM_DB=1
+//    Cfg<256, 128, 64> with TWO 72 KB stages -- chunk c + 1 is split into
+//    planes and written to one stage while chunk c's MFMAs run from fragments
+//    already read out of the other, one barrier per chunk.  Measured at
+//    N = 100k, D = 256 (tools/gpu_nce_ab.sh): fwd 31.8 vs 29.2 ms, ranks 28.6
+//    vs 24.4 ms -- with K = 256 a block runs only 8 chunks, so the halved tile
+//    pays its prologue / epilogue twice as often and splits 1.5x the operand
+//    floats per output (1.4 VALU per MFMA, beyond the 2 issue slots an MFMA
+//    leaves once address math is counted).
+// Every element's K order and six-product order are the same in both, so the
+// similarity values (and k_nce_diag's replay of them) are bitwise unchanged.
+template <int BM_, int BN_, int WN_> struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WN = WN_, TN = WN_ / 16;
+  static constexpr int NWM = BM_ / WM, NWN = BN_ / WN_, NW = NWM * NWN, NTH = NW * 64;
+  static_assert(NW == 8, "8 waves");
 };
-using BlkSim = Blk<TT_NCE_SIM_BM>;
-using BlkGrad = Blk<256>;
+#ifndef TT_NCE_SIM_DB
+#define TT_NCE_SIM_DB 0
+#endif
+#if TT_NCE_SIM_DB
+using CfgSim = Cfg<256, 128, 64>;
+#else
+using CfgSim = Cfg<256, 256, 128>;
+#endif
+using CfgGrad = Cfg<256, 256, 128>;
 constexpr int TILE = 256;                                    // floats per 16x16 tile
 constexpr float SUM_MIN = 1e-30f;  // row/col sums below this: exp underflow (reported)
 
@@ -78,12 +89,12 @@ __device__ __forceinline__ int lds_off(int m, int k) {  // bf16 offset of (m, k)
   if constexpr (SWZ) return m * Lay<SWZ, 1>::LDK + ((((k >> 3) ^ lds_swz(m)) << 3) | (k & 7));
   else return m * Lay<SWZ, 1>::LDK + k;
 }
-// A (BM rows) + B (BN rows), single stage
-template <int BM_, bool SWZ>
-constexpr size_t lds_bytes() { return sizeof(uint16_t) * (Lay<SWZ, BM_>::OPND + Lay<SWZ, BN>::OPND); }
-constexpr size_t LDS_SIM = lds_bytes<BlkSim::BM, true>();     // 96 KB (72 KB at BM 128); both operands SRC_MK
-constexpr size_t LDS_GRAD = lds_bytes<BlkGrad::BM, false>();  // 120 KB
-static_assert(BlkSim::MIN_WAVES == 1 || 2 * LDS_SIM <= 160 * 1024, "two similarity blocks per CU");
+// one stage = A (BM rows) + B (BN rows), in bf16 elements
+template <class C, bool SWZ>
+constexpr int stage_elems() { return Lay<SWZ, C::BM>::OPND + Lay<SWZ, C::BN>::OPND; }
+constexpr size_t LDS_SIM = sizeof(uint16_t) * (TT_NCE_SIM_DB ? 2 : 1) * stage_elems<CfgSim, true>();  // 96 / 144 KB
+constexpr size_t LDS_GRAD = sizeof(uint16_t) * stage_elems<CfgGrad, false>();                        // 120 KB
+static_assert(LDS_SIM <= 160 * 1024 && LDS_GRAD <= 160 * 1024, "LDS per CU");
 
 
 // Where an operand comes from.  LDS always holds [m][k] bf16 planes.
@@ -130,7 +141,7 @@ struct GemmArgs {
   const float* shift;  // device scalar
   float* E;            // tiles [nti][ntj][256]
   int64_t e_nti, e_ntj;
-  float* rowpart;      // [N / WN parts][M_pad]
+  float* rowpart;      // [N / WN parts][M_pad] (WN of CfgSim)
   float* colpart;      // [M / WM parts][N_pad]
   int64_t m_pad, n_pad;
   int64_t row0;        // global index of local row 0 (diagonal j == row0 + i)
@@ -297,14 +308,14 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* L, int plane, int m, int 
 
 
 // Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T.  One LDS
-// stage (120 KB); the next chunk's global loads are in flight during the
-// MFMAs of the current one.
-template <int SA, int SB, int BM_>
+// stage; the next chunk's global loads are in flight during the MFMAs of the
+// current one.
+template <int SA, int SB, class C>
 __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
-                                          uint16_t* smem, f32x4 (&acc)[TM][TN]) {
-  constexpr int NT = Blk<BM_>::NTH;
+                                          uint16_t* smem, f32x4 (&acc)[TM][C::TN]) {
+  constexpr int NT = C::NTH, BM_ = C::BM, BN = C::BN, TN = C::TN, WN = C::WN;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  const int wm = w / NWN, wn = w % NWN;
+  const int wm = w / C::NWN, wn = w % C::NWN;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -344,6 +355,69 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
   }
 }
 
+// Double-buffered main loop of the similarity kernels (both operands SRC_MK,
+// swizzled LDS): stage c & 1 holds chunk c, the registers chunk c + 1.  Each
+// iteration reads all of chunk c's fragments (24 x 16 B per lane), then splits
+// and writes chunk c + 1 into the other stage and issues chunk c + 2's loads --
+// VALU and LDS writes the scheduler interleaves with chunk c's 96 MFMAs, which
+// depend only on registers -- and ends with the one barrier.  Loads past K
+// return zeros (buffer range), so the body has no branches.
+template <class C>
+__device__ __forceinline__ void gemm_loop_db(const GemmArgs& g_, int64_t m0, int64_t n0, uint16_t* smem,
+                                             f32x4 (&acc)[TM][C::TN]) {
+  constexpr int NT = C::NTH, TN = C::TN;
+  constexpr int AOP = Lay<true, C::BM>::OPND, STAGE = stage_elems<C, true>();
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
+  const int wm = w / C::NWN, wn = w % C::NWN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  const int nch = (int)((g_.A.kdim + BK - 1) / BK);
+  if (nch <= 0) return;
+  float4 va[C::BM * 8 / NT], vb[C::BN * 8 / NT];
+  auto fetch = [&](int c) {
+    load_opnd<SRC_MK, C::BM, NT>(g_.A, m0, (int64_t)c * BK, va);
+    load_opnd<SRC_MK, C::BN, NT>(g_.B, n0, (int64_t)c * BK, vb);
+  };
+  auto put = [&](uint16_t* S) {
+    store_opnd<SRC_MK, true, C::BM, NT>(S, va);
+    store_opnd<SRC_MK, true, C::BN, NT>(S + AOP, vb);
+  };
+  bf16x8 a[TM][NPL], b[TN][NPL];
+  auto frags = [&](const uint16_t* S) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) a[i][p] = frag<true, C::BM>(S, p, wm * WM + 16 * i + r, g);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) b[j][p] = frag<true, C::BN>(S + AOP, p, wn * C::WN + 16 * j + r, g);
+  };
+  auto mma = [&]() {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = mfma_bf16(a[i][PA[q]], b[j][PB[q]], acc[i][j]);
+  };
+  fetch(0);
+  put(smem);
+  fetch(1);
+  __syncthreads();
+  for (int c = 0; c + 1 < nch; ++c) {
+    frags(smem + (c & 1) * STAGE);
+    put(smem + ((c + 1) & 1) * STAGE);  // its readers (chunk c - 1) passed the last barrier
+    fetch(c + 2);
+    mma();
+    __syncthreads();
+  }
+  frags(smem + ((nch - 1) & 1) * STAGE);
+  mma();
+}
+
 // XCD-aware block order: consecutive block ids land on different XCDs
 // (round robin); remap so each XCD walks a compact run of the tile grid
 // (shared A/B panels stay in its L2).
@@ -358,15 +432,20 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t nblk) {
 // k_nce_sim: S = F C^T (MODE 0: InfoNCE exp/partials; MODE 1: rank counts)
 // ---------------------------------------------------------------------------
 template <int MODE>
-__global__ __launch_bounds__(BlkSim::NTH, BlkSim::MIN_WAVES) void k_nce_sim(GemmArgs a) {
+__global__ __launch_bounds__(CfgSim::NTH) void k_nce_sim(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int NWM = BlkSim::NWM;
+  using C = CfgSim;
+  constexpr int NWM = C::NWM, NWN = C::NWN, TN = C::TN, WN = C::WN;
   const int64_t nblk = (int64_t)gridDim.x;
   const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
   const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
-  const int64_t m0 = bm * BlkSim::BM, n0 = bn * BN;
+  const int64_t m0 = bm * C::BM, n0 = bn * C::BN;
   f32x4 acc[TM][TN];
-  gemm_loop<SRC_MK, SRC_MK, BlkSim::BM>(a, m0, n0, 0, a.A.kdim, smem, acc);
+#if TT_NCE_SIM_DB
+  gemm_loop_db<C>(a, m0, n0, smem, acc);
+#else
+  gemm_loop<SRC_MK, SRC_MK, C>(a, m0, n0, 0, a.A.kdim, smem, acc);
+#endif
 
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   const int wm = w / NWN, wn = w % NWN;
@@ -521,17 +600,19 @@ __global__ __launch_bounds__(256) void k_nce_diag(const float* __restrict__ F, c
 // accumulator-layout tiles part[split][ti][tj][256]
 // ---------------------------------------------------------------------------
 template <int SA>
-__global__ __launch_bounds__(BlkGrad::NTH) void k_nce_dgrad(GemmArgs a) {
+__global__ __launch_bounds__(CfgGrad::NTH) void k_nce_dgrad(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  using C = CfgGrad;
+  constexpr int NWN = C::NWN, TN = C::TN, WN = C::WN;
   const int64_t nblk = (int64_t)gridDim.x;
   const int64_t bid = xcd_swizzle(blockIdx.x, nblk);
   const int64_t bm = bid / a.n_blocks_n, bn = bid % a.n_blocks_n;
-  const int64_t m0 = bm * BlkGrad::BM, n0 = bn * BN;
+  const int64_t m0 = bm * C::BM, n0 = bn * C::BN;
   const int64_t split = blockIdx.y;
   const int64_t kb = split * a.k_per_split;
   const int64_t ke = min(kb + a.k_per_split, a.A.kdim);
   f32x4 acc[TM][TN];
-  gemm_loop<SA, SRC_KROWS, BlkGrad::BM>(a, m0, n0, kb, ke, smem, acc);
+  gemm_loop<SA, SRC_KROWS, C>(a, m0, n0, kb, ke, smem, acc);
   const int w = wave_id(), l = lane_id();
   const int wm = w / NWN, wn = w % NWN;
 #pragma unroll

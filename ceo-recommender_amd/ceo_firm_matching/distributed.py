@@ -96,12 +96,17 @@ class PeerExchange:
         dist.all_gather_object(where, (socket.gethostname(), torch.device(device).index or 0), group=group)
         if len(set(where)) < world and world > 2 and mode != "1":
             return None
+        if len({h for h, _ in where}) > 1:  # IPC handles do not cross hosts
+            return None
         ok = torch.ones(1, dtype=torch.int32, device=flag_dev)
-        ex = None
-        try:
-            ex = PeerExchange._map(n, group, device, rank, world)
-        except Exception:  # noqa: BLE001 -- any setup failure keeps the collective
+        if not PeerExchange._peers_reachable(where, rank):
             ok.zero_()
+        ex = None
+        if int(ok.item()):
+            try:
+                ex = PeerExchange._map(n, group, device, rank, world)
+            except Exception:  # noqa: BLE001 -- any setup failure keeps the collective
+                ok.zero_()
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # every rank mapped, or none uses it
         if int(ok.item()) == 0:
             if ex is not None:
@@ -121,6 +126,17 @@ class PeerExchange:
             return None
         ex.reset(group)
         return ex
+
+    @staticmethod
+    def _peers_reachable(where, rank) -> bool:
+        """Every other rank's device is this rank's own or one its kernels
+        can address directly (xGMI / PCIe peer access): the exchange kernel
+        reads and writes the peers' regions from the device."""
+        mine = where[rank][1]
+        try:
+            return all(d == mine or torch.cuda.can_device_access_peer(mine, d) for _, d in where)
+        except Exception:  # noqa: BLE001 -- unknown topology keeps the collective
+            return False
 
     @staticmethod
     def _map(n, group, device, rank, world):

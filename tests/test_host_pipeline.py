@@ -124,3 +124,14 @@ def test_peer_exchange_not_used_without_a_group():
     from ceo_firm_matching.distributed import PeerExchange
     assert PeerExchange.create(100, None, "cpu") is None
     assert PeerExchange.create(100, None, "cpu", mode="0") is None
+
+
+def test_peer_exchange_reachability_rule():
+    """The exchange is only mapped when every peer's device is this rank's
+    own or one it can address directly; a topology query that fails (no GPU
+    here) keeps the collective."""
+    from ceo_firm_matching.distributed import PeerExchange
+    same = [("h", 0), ("h", 0)]
+    assert PeerExchange._peers_reachable(same, 0) and PeerExchange._peers_reachable(same, 1)
+    if not torch.cuda.is_available():
+        assert not PeerExchange._peers_reachable([("h", 0), ("h", 1)], 0)

@@ -284,3 +284,52 @@ def test_semi_hard_row_shards_compose():
     assert torch.equal(torch.cat([p[1] for p in parts]), hardest)
     assert torch.equal(torch.cat([p[2] for p in parts]), row_loss)
     assert abs(float(sum(p[0] for p in parts)) - float(loss.detach())) <= TOL * float(loss.detach())
+
+
+def _info_nce_fp64_chunked(f, c, tau, chunk=8192):
+    """Symmetric InfoNCE (contrastive.py:102-138) and its gradients in fp64
+    on the device, in row chunks (never the whole N x N): a plain torch
+    reference for the full cfg-5 size, where the CPU oracle is too slow."""
+    f, c = f.double(), c.double()
+    n = f.shape[0]
+    shift = 1.0 / tau  # unit rows: |S| <= 1 / tau
+    rowsum = torch.empty(n, dtype=torch.float64, device=f.device)
+    colsum = torch.zeros(n, dtype=torch.float64, device=f.device)
+    for i0 in range(0, n, chunk):
+        e = torch.exp(f[i0:i0 + chunk] @ c.T / tau - shift)
+        rowsum[i0:i0 + chunk] = e.sum(1)
+        colsum += e.sum(0)
+    diag = (f * c).sum(1) / tau
+    lse_r, lse_c = torch.log(rowsum) + shift, torch.log(colsum) + shift
+    loss = 0.5 * ((lse_r - diag).mean() + (lse_c - diag).mean())
+    df = torch.empty_like(f)
+    dc = torch.zeros_like(c)
+    for i0 in range(0, n, chunk):
+        i1 = min(i0 + chunk, n)
+        g = torch.exp(f[i0:i1] @ c.T / tau - shift)
+        g *= (1.0 / rowsum[i0:i1])[:, None] + (1.0 / colsum)[None, :]
+        df[i0:i1] = g @ c
+        dc += g.T @ f[i0:i1]
+        del g
+    df = df / (2 * n * tau) - c / (n * tau)
+    dc = dc / (2 * n * tau) - f / (n * tau)
+    return float(loss), df, dc
+
+
+def test_info_nce_full_cfg5_vs_fp64():
+    """BASELINE cfg 5 at its full size (100k firms x 100k CEOs, D = 256, the
+    bench's workload): loss and both gradients vs an fp64 device reference,
+    1e-5 (loss relative, gradients normwise)."""
+    dev = _dev()
+    n, d, tau = 100_000, 256, 0.07
+    gen = torch.Generator(device=dev).manual_seed(5)
+    f = torch.nn.functional.normalize(torch.randn(n, d, device=dev, generator=gen), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(n, d, device=dev, generator=gen) + 0.3 * f, dim=1)
+    loss, df, dc = _nce(f, c, tau)
+    loss = float(loss.detach())
+    torch.cuda.empty_cache()  # the similarity workspace (40 GB) before the reference's chunks
+    rl, rdf, rdc = _info_nce_fp64_chunked(f, c, tau)
+    assert abs(loss - rl) <= TOL * abs(rl), (loss, rl)
+    for got, ref in ((df, rdf), (dc, rdc)):
+        err = float((got.double() - ref).abs().max() / ref.abs().max())
+        assert err < TOL, err

@@ -564,6 +564,9 @@ __device__ __forceinline__ float tower_x(const TowerDev& T, int64_t drow, int co
 // gradient reduction / Adam arguments (tt_optim.hip)
 // ---------------------------------------------------------------------------
 constexpr int MAX_SEG = 48;
+#ifndef TT_RED_MINW
+#define TT_RED_MINW 8  // waves per SIMD: <= 64 VGPRs, 4 blocks of 512 per CU (every block resident); 8.50 -> 8.25 us
+#endif
 #ifndef TT_RED_E
 #define TT_RED_E 32
 #endif

@@ -39,9 +39,11 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   p = p + (-c.step_size) * (m / denom);
 }
 
-__global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
+__global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedArgs a) {
   __shared__ float part[RED_G][RED_E];
   TT_STAMP(5, 0);
+  // the step first: a later load would make its wait (in-order vmcnt) wait for the slabs
+  const int64_t t = a.state ? a.state->step_cur : a.step_host;
   const int el = threadIdx.x & (RED_E - 1), pg = threadIdx.x / RED_E;
   const int64_t e = (int64_t)blockIdx.x * RED_E + el;
   int si = -1;
@@ -57,6 +59,14 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
     pv = a.v[e];
   }
   float acc = 0.f;
+  // Adam's bias corrections (double pow: a long dependent chain) are computed
+  // by the owner lanes between issuing the slab loads and summing them (was:
+  // after the barrier, on the critical path; 8.2 -> 7.3 us).  Owner lanes
+  // only: the same pow in every wave costs more (11.4 us) than it hides.
+  // (The code shape matters: an equivalent lambda form measured 10.1 us.)
+  AdamCoef c{};
+  const bool adam_here = owner && a.apply_adam;
+  bool coef_done = false;
   if (si >= 0) {
     const Seg& S = a.seg[si];
     if (S.kind == 0) {
@@ -70,6 +80,10 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
         for (int k = 0; k < UNR; ++k) {
           const int p = min(p0 + k * RED_G, n - 1);
           v[k] = base[(int64_t)p * a.slab_ld];
+        }
+        if (!coef_done) {
+          if (adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+          coef_done = true;
         }
 #pragma unroll
         for (int k = 0; k < UNR; ++k) acc += (p0 + k * RED_G < n) ? v[k] : 0.f;
@@ -85,6 +99,7 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
       }
     }
   }
+  if (!coef_done && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
   part[pg][el] = acc;
   // zero the BN moment sums consumed by this step (one element per thread of
   // the leading blocks); fold the loss replicas (block 0)
@@ -115,8 +130,6 @@ __global__ __launch_bounds__(RED_E* RED_G) void k_reduce_adam(RedArgs a) {
   a.grad[e] = gsum;
   if (a.seg[si].kind == 1) a.gacc[e] = 0.f;
   if (a.apply_adam) {
-    const int64_t t = a.state ? a.state->step_cur : a.step_host;
-    const AdamCoef c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
     adam_elem(pp, pm, pv, gsum, c);
     a.p[e] = pp;
     a.m[e] = pm;

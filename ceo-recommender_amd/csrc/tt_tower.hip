@@ -43,30 +43,36 @@ namespace tt {
 // eval: running stats).  `update`: fold the batch stats into the running
 // estimates (momentum, unbiased variance, torch semantics) and publish
 // mean|invstd for the backward kernels.
-__device__ __forceinline__ void bn_coefs(const StepArgs& a, int H, const float* st, const float* shift,
-                                         float* rm, float* rv, int64_t* nbt, float* fin, bool update,
-                                         int c, float* mean_out, float* inv_out) {
+// (bn_coefs_pre: the same on shift[c], rm[c], rv[c] loaded by the caller)
+__device__ __forceinline__ void bn_coefs_pre(const StepArgs& a, int H, const float* st, float shift_c, float rm_c,
+                                             float rv_c, float* rm, float* rv, int64_t* nbt, float* fin,
+                                             bool update, int c, float* mean_out, float* inv_out) {
   float mean, var;
   if (a.train) {
     const double Bd = (double)a.B;
     const float m1 = st[c] / (float)Bd;  // st: replica-summed S1|S2 (LDS)
     var = st[H + c] / (float)Bd - m1 * m1;
     var = var < 0.f ? 0.f : var;
-    mean = shift[c] + m1;
+    mean = shift_c + m1;
     if (update) {
       const float mom = a.momentum;
-      rm[c] = (1.f - mom) * rm[c] + mom * mean;
-      rv[c] = (1.f - mom) * rv[c] + mom * (var * (float)(Bd / (Bd - 1.0)));
+      rm[c] = (1.f - mom) * rm_c + mom * mean;
+      rv[c] = (1.f - mom) * rv_c + mom * (var * (float)(Bd / (Bd - 1.0)));
       fin[c] = mean;
       fin[H + c] = 1.f / sqrtf(var + a.eps);
       if (c == 0) *nbt += 1;
     }
   } else {
-    mean = rm[c];
-    var = rv[c];
+    mean = rm_c;
+    var = rv_c;
   }
   *mean_out = mean;
   *inv_out = 1.f / sqrtf(var + a.eps);
+}
+__device__ __forceinline__ void bn_coefs(const StepArgs& a, int H, const float* st, const float* shift,
+                                         float* rm, float* rv, int64_t* nbt, float* fin, bool update,
+                                         int c, float* mean_out, float* inv_out) {
+  bn_coefs_pre(a, H, st, shift[c], rm[c], rv[c], rm, rv, nbt, fin, update, c, mean_out, inv_out);
 }
 
 // BN apply + ReLU + (train) dropout of one element.
@@ -122,13 +128,13 @@ struct RepSum2 {
   static_assert(NTH % N2 == 0 && NREP % G == 0, "replica groups");
   float v[PER];
   __device__ __forceinline__ void issue(const float* rep0, const float* rep1, int stride) {
-    const int c2 = (int)threadIdx.x % N2, grp = (int)threadIdx.x / N2;
-    if (grp < G) {
-      const float* rep = c2 < N ? rep0 : rep1;
-      const int c = c2 < N ? c2 : c2 - N;
+    // every thread loads (groups beyond G re-read group G - 1, ignored by
+    // finish): no branch join that would make hipcc wait for the loads here
+    const int c2 = (int)threadIdx.x % N2, grp = min((int)threadIdx.x / N2, G - 1);
+    const float* rep = c2 < N ? rep0 : rep1;
+    const int c = c2 < N ? c2 : c2 - N;
 #pragma unroll
-      for (int k = 0; k < PER; ++k) v[k] = rep[(grp + k * G) * stride + c];
-    }
+    for (int k = 0; k < PER; ++k) v[k] = rep[(grp + k * G) * stride + c];
   }
   __device__ __forceinline__ void finish(float* scratch, float* dst) {
     const int c2 = (int)threadIdx.x % N2, grp = (int)threadIdx.x / N2;
@@ -681,14 +687,14 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     bs = a.tw[own].b8[d];
   }
   const float lsc = *a.logit_scale;
-  float tg = 0.f, wt = 0.f;
-  if (a.mode == TOP_TRAIN) {
-    const float2 v = *reinterpret_cast<const float2*>(a.tgw + 2 * row);
-    tg = v.x;
-    wt = v.y;
-  } else if (a.mode == TOP_BWD_GIVEN) {
-    tg = a.dscore[min(row, a.B - 1)];
-  }
+  // this row's (target, weight) or dscore: loads from a valid address in
+  // every mode, no branch -- a load under one arm of a branch made hipcc
+  // drain vmcnt at the join, before the replica loads below were issued
+  const bool m_train = a.mode == TOP_TRAIN, m_given = a.mode == TOP_BWD_GIVEN;
+  const float* p_tg = m_train ? a.tgw + 2 * row : (m_given ? a.dscore + min(row, a.B - 1) : a.logit_scale);
+  const float* p_wt = m_train ? a.tgw + 2 * row + 1 : a.logit_scale;
+  const float tg_raw = *p_tg, wt_raw = *p_wt;
+  const float tg = (m_train || m_given) ? tg_raw : 0.f, wt = m_train ? wt_raw : 0.f;
   f32x4 dem[EMB ? NDT : 1];  // TOP_EMB_BWD: this lane's dU slice (issued with the other loads)
   if constexpr (EMB) {
     if (bwd) {
@@ -698,6 +704,25 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) dem[j][i] = src[min(16 * j + 4 * g + i, D - 1)];
     }
+  }
+  // BN1 parameters of column bc of tower bt (wave 0: threads < 2 H1), issued
+  // with the other loads; the per-lane tower's pointers are selected from
+  // both towers' (scalar) kernel arguments -- a.tw[lane-dependent] would be a
+  // vector load of the argument block, then a second dependent round trip
+  const int bt = ((int)threadIdx.x / H1) & 1, bc = (int)threadIdx.x % H1;
+  auto pick = [&](auto p0, auto p1) { return bt ? p1 : p0; };
+  float bn_sh = 0.f, bn_rm = 0.f, bn_rv = 0.f, bn_g = 0.f, bn_be = 0.f;
+  if (w == 0) {
+    // running stats are NULL when the caller passes no buffers (backward):
+    // read gamma in their place then (never used: bn_coefs_pre reads them
+    // only for eval or a statistics update, which come with buffers)
+    const bool have_rs = a.tw[0].rm1 != nullptr;
+    const float* g1p = pick(a.tw[0].g1, a.tw[1].g1);
+    bn_sh = pick(a.tw[0].shift1, a.tw[1].shift1)[bc];
+    bn_rm = (have_rs ? pick(a.tw[0].rm1, a.tw[1].rm1) : g1p)[bc];
+    bn_rv = (have_rs ? pick(a.tw[0].rv1, a.tw[1].rv1) : g1p)[bc];
+    bn_g = g1p[bc];
+    bn_be = pick(a.tw[0].be1, a.tw[1].be1)[bc];
   }
   RepSum2<NTH, 2 * H1> rs;
   if (a.train) rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
@@ -720,16 +745,18 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     }
   }
   if (a.train) rs.finish(smem + L::rsc, smem + L::rst);
+  static_assert(2 * H1 <= 64, "BN1 coefficients: wave 0");
   if (threadIdx.x < 2 * H1) {
-    const int tau = threadIdx.x / H1, c = threadIdx.x % H1;
-    const TowerDev& T = a.tw[tau];
+    const int tau = bt, c = bc;
     const bool upd = a.update_stats && blockIdx.x == 0 && (bwd ? tau == own : true);
     float mean, inv;
-    bn_coefs(a, H1, smem + L::rst + tau * 2 * H1, T.shift1, T.rm1, T.rv1, T.nbt1, T.fin1, upd, c, &mean, &inv);
+    bn_coefs_pre(a, H1, smem + L::rst + tau * 2 * H1, bn_sh, bn_rm, bn_rv, pick(a.tw[0].rm1, a.tw[1].rm1),
+                 pick(a.tw[0].rv1, a.tw[1].rv1), pick(a.tw[0].nbt1, a.tw[1].nbt1), pick(a.tw[0].fin1, a.tw[1].fin1),
+                 upd, c, &mean, &inv);
     float* cf = smem + L::cf1 + tau * 4 * H1;
     cf[c] = mean;
-    cf[H1 + c] = inv * T.g1[c];
-    cf[2 * H1 + c] = T.be1[c];
+    cf[H1 + c] = inv * bn_g;
+    cf[2 * H1 + c] = bn_be;
     cf[3 * H1 + c] = inv;
   }
   __syncthreads();

@@ -492,19 +492,37 @@ __global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
   float bias[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias[j] = T.b4[16 * j + r];
-  const float z0r = threadIdx.x < H0 ? T.Z0[threadIdx.x] : 0.f;
+  const float z0r_raw = T.Z0[min((int)threadIdx.x, H0 - 1)];
+  const float z0r = threadIdx.x < H0 ? z0r_raw : 0.f;
+  // W4 (raw) and wave 0's BN0 parameters are issued with the Z0 loads: one
+  // round trip for the whole phase (they used to follow the replica sum)
+  static_assert(H1 * H0 / 4 == 2 * NTH && H0 == 64, "W4: 2 float4 per thread; BN0: wave 0");
+  const int we0 = (int)threadIdx.x, we1 = (int)threadIdx.x + NTH;  // two float4 per thread (named: no array)
+  const float4 w4a = *reinterpret_cast<const float4*>(T.W4 + (we0 >> 4) * H0 + 4 * (we0 & 15));
+  const float4 w4b = *reinterpret_cast<const float4*>(T.W4 + (we1 >> 4) * H0 + 4 * (we1 & 15));
+  float bn_sh = 0.f, bn_rm = 0.f, bn_rv = 0.f, bn_g = 0.f, bn_be = 0.f;
+  if (w == 0) {
+    const float* rmp = T.rm0 ? T.rm0 : T.g0;  // running stats NULL without buffers (never read then)
+    const float* rvp = T.rv0 ? T.rv0 : T.g0;
+    bn_sh = T.shift0[l];
+    bn_rm = rmp[l];
+    bn_rv = rvp[l];
+    bn_g = T.g0[l];
+    bn_be = T.be0[l];
+  }
   if (a.train) rep_sum<NTH, 2 * H0>(T.st0, 2 * H0, rsc, rst);
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
     float mean, inv;
-    bn_coefs(a, H0, rst, T.shift0, T.rm0, T.rv0, T.nbt0, T.fin0, a.update_stats && blockIdx.x == 0, c, &mean,
-             &inv);
+    bn_coefs_pre(a, H0, rst, bn_sh, bn_rm, bn_rv, T.rm0, T.rv0, T.nbt0, T.fin0, a.update_stats && blockIdx.x == 0,
+                 c, &mean, &inv);
     cf[c] = mean;
-    cf[H0 + c] = inv * T.g0[c];
-    cf[2 * H0 + c] = T.be0[c];
+    cf[H0 + c] = inv * bn_g;
+    cf[2 * H0 + c] = bn_be;
   }
   if (threadIdx.x < 2 * H1) red[threadIdx.x] = 0.f;
-  g2s_f4<NTH, 2>(T.W4, H0, W4s, LD, H1, H0);
+  *reinterpret_cast<float4*>(W4s + (we0 >> 4) * LD + 4 * (we0 & 15)) = w4a;
+  *reinterpret_cast<float4*>(W4s + (we1 >> 4) * LD + 4 * (we1 & 15)) = w4b;
   __syncthreads();
   TT_STAMP(1, 1);
 

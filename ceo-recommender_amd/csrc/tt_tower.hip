@@ -1086,27 +1086,36 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) zz0[j][i] = T.Z0[row * H0 + 16 * j + r];
   }
+  // W4 and the BN coefficients' inputs are issued with the tiles above (one
+  // round trip; they used to follow the replica sum, W4 in two dependent
+  // load -> store pairs).  Every thread loads (clamped columns): no branch.
+  static_assert(H1 * H0 / 4 == 2 * NTH, "W4: 2 float4 per thread");
+  const int we0 = (int)threadIdx.x, we1 = (int)threadIdx.x + NTH;
+  const float4 w4a = *reinterpret_cast<const float4*>(T.W4 + (we0 >> 4) * H0 + 4 * (we0 & 15));
+  const float4 w4b = *reinterpret_cast<const float4*>(T.W4 + (we1 >> 4) * H0 + 4 * (we1 & 15));
+  const int c1i = min((int)threadIdx.x, H1 - 1), c0i = min(max((int)threadIdx.x - H1, 0), H0 - 1);
+  const float f1inv = T.fin1[H1 + c1i], f1mean = T.fin1[c1i], g1v = T.g1[c1i];
+  const float f0inv = T.fin0[H0 + c0i], f0mean = T.fin0[c0i], g0v = T.g0[c0i], be0v = T.be0[c0i];
   const float invB = 1.f / (float)a.B;
   rep_sum<NTH, 2 * H1>(T.gg1, BNG, rsc, rst);  // gg1|gbe1 are adjacent in a replica
   if (threadIdx.x < H1) {
     const int c = threadIdx.x;
-    const float inv = T.fin1[H1 + c];
-    c1[c] = inv * T.g1[c];
+    c1[c] = f1inv * g1v;
     c1[H1 + c] = rst[H1 + c] * invB;
     c1[2 * H1 + c] = rst[c] * invB;
-    c1[3 * H1 + c] = T.fin1[c];
-    c1[4 * H1 + c] = inv;
+    c1[3 * H1 + c] = f1mean;
+    c1[4 * H1 + c] = f1inv;
   } else if (threadIdx.x < H1 + H0) {
     const int c = threadIdx.x - H1;
-    const float inv = T.fin0[H0 + c];
-    c0[c] = T.fin0[c];
-    c0[H0 + c] = inv * T.g0[c];
-    c0[2 * H0 + c] = T.be0[c];
-    c0[3 * H0 + c] = inv;
+    c0[c] = f0mean;
+    c0[H0 + c] = f0inv * g0v;
+    c0[2 * H0 + c] = be0v;
+    c0[3 * H0 + c] = f0inv;
   }
   if (threadIdx.x < H1) db4[threadIdx.x] = 0.f;
   if (threadIdx.x < 2 * H0) red[threadIdx.x] = 0.f;
-  g2s_f4<NTH, 2>(T.W4, H0, W4s, LDW, H1, H0);
+  *reinterpret_cast<float4*>(W4s + (we0 >> 4) * LDW + 4 * (we0 & 15)) = w4a;
+  *reinterpret_cast<float4*>(W4s + (we1 >> 4) * LDW + 4 * (we1 & 15)) = w4b;
   __syncthreads();
   TT_STAMP(3, 1);
 
@@ -1232,6 +1241,12 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   float* rst = rsc + NTH;                              // [2*64] sum dgamma0 | sum dbeta0
   TT_STAMP(4, 0);
 
+  // Phase 0 issues every load before its first wait: this tile's dataset
+  // rows (first: the X gather after the barrier depends on them), the dY0 /
+  // Z0 tiles, BN0's inputs (every thread, clamped column: no branch) and the
+  // replica loads inside rep_sum; the row indices reach LDS after rep_sum's
+  // wait (a store right after their load would wait for the tiles too).
+  const int64_t my_row = data_row_nb(a, base, min(r0 + (int64_t)(threadIdx.x % R), a.B - 1));
   f32x4 dy0[4], zz0[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1242,17 +1257,18 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
       zz0[j][i] = T.Z0[row * H0 + 16 * j + r];
     }
   }
-  stage_ridx<R>(a, base, r0, ridx);
+  const int cc = (int)threadIdx.x % H0;
+  const float f0inv = T.fin0[H0 + cc], f0mean = T.fin0[cc], g0v = T.g0[cc];
   const float invB = 1.f / (float)a.B;
   rep_sum<NTH, 2 * H0>(T.gg0, BNG, rsc, rst);  // gg0|gbe0 are adjacent in a replica
+  if (threadIdx.x < R) ridx[threadIdx.x] = my_row;
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
-    const float inv = T.fin0[H0 + c];
-    c0[c] = inv * T.g0[c];
+    c0[c] = f0inv * g0v;
     c0[H0 + c] = rst[H0 + c] * invB;
     c0[2 * H0 + c] = rst[c] * invB;
-    c0[3 * H0 + c] = T.fin0[c];
-    c0[4 * H0 + c] = inv;
+    c0[3 * H0 + c] = f0mean;
+    c0[4 * H0 + c] = f0inv;
     db0[c] = 0.f;
   }
   __syncthreads();

@@ -189,14 +189,15 @@ __device__ __forceinline__ uint64_t row_min16(uint64_t v) {
 template <int S, int ROWS, int NT>
 __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0, float4 (&v)[ROWS * 8 / NT]) {
   constexpr int NQ = ROWS * 8 / NT;
-  if constexpr (S == SRC_MK) {  // tile ROWS x BK from G[m][k]: 8 float4 per row
+  if constexpr (S == SRC_MK) {  // tile ROWS x BK from G[m][k]: 4 k-octets (2 float4) per row
     const auto rs = buf_rsrc(o.p + m0 * o.ld, (o.mdim - m0) * o.ld * 4);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int e = (int)threadIdx.x + q * NT;
-      const int r = e >> 3, kq = (e & 7) * 4;
-      const bool ok = k0 + kq < o.kdim;
-      v[q] = buf_f32x4(rs, ok ? (uint32_t)((r * o.ld + k0 + kq) * 4) : BUF_OOB);
+    for (int t = 0; t < NQ / 2; ++t) {
+      const int e = (int)threadIdx.x + t * NT;
+      const int r = e >> 2, k8 = (e & 3) * 8;
+      const bool ok0 = k0 + k8 < o.kdim, ok1 = k0 + k8 + 4 < o.kdim;
+      v[2 * t] = buf_f32x4(rs, ok0 ? (uint32_t)((r * o.ld + k0 + k8) * 4) : BUF_OOB);
+      v[2 * t + 1] = buf_f32x4(rs, ok1 ? (uint32_t)((r * o.ld + k0 + k8 + 4) * 4) : BUF_OOB);
     }
   } else if constexpr (S == SRC_KROWS) {  // G[k][m]: ROWS m (lanes) x 4 k-octets, 8 scalar loads
     // (an item is 8 consecutive k = one 16-B LDS granule per plane, v[2t] | v[2t + 1])
@@ -258,14 +259,17 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
 template <int S, bool SWZ, int ROWS, int NT>
 __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[ROWS * 8 / NT]) {
   constexpr int PLANE = Lay<SWZ, ROWS>::PLANE;
-  if constexpr (S == SRC_KROWS) {
-    // lanes run along m at one k-octet: 16-B writes of 80-B rows hit 16
-    // distinct 16-B slots per 16 lanes (8-B writes of 4 k would pair rows
-    // m and m + 16 on one bank: 2-way conflicts)
+  if constexpr (S == SRC_KROWS || S == SRC_MK) {
+    // one k-octet per item: a 16-B granule per plane.  SRC_KROWS: lanes run
+    // along m at one octet -- 16-B writes of 80-B rows hit 16 distinct 16-B
+    // slots per 16 lanes (8-B writes of 4 k would pair rows m and m + 16 on
+    // one bank); SRC_MK: 4 lanes per 64-B swizzled row, 16 lanes = 256 B.
+    // Half the write instructions of 8-B plane writes.
 #pragma unroll
     for (int t = 0; t < ROWS * 4 / NT; ++t) {
       const int e = (int)threadIdx.x + t * NT;
-      const int m = e % ROWS, k8 = (e / ROWS) * 8;
+      const int m = S == SRC_KROWS ? e % ROWS : e >> 2;
+      const int k8 = S == SRC_KROWS ? (e / ROWS) * 8 : (e & 3) * 8;
       const float x[8] = {v[2 * t].x,     v[2 * t].y,     v[2 * t].z,     v[2 * t].w,
                           v[2 * t + 1].x, v[2 * t + 1].y, v[2 * t + 1].z, v[2 * t + 1].w};
       bf16x8 pl[NPL];
@@ -281,9 +285,7 @@ __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[ROWS *
   for (int q = 0; q < ROWS * 8 / NT; ++q) {
     const int e = (int)threadIdx.x + q * NT;
     int m, k;  // the thread's float4 holds k .. k+3 of row m
-    if constexpr (S == SRC_MK) {
-      m = e >> 3; k = (e & 7) * 4;
-    } else if constexpr (S == SRC_E_ROWS) {  // quad-transposed tile float4: row i, 4 consecutive j
+    if constexpr (S == SRC_E_ROWS) {  // quad-transposed tile float4: row i, 4 consecutive j
       const int t = e >> 6, ln = e & 63, tm = t >> 1, tk = t & 1;
       m = 16 * tm + 4 * (ln >> 4) + (ln & 3); k = 16 * tk + (ln & 12);
     } else {  // SRC_E_AS_MK: the tile float4 = 4 consecutive E rows i = k

@@ -6,8 +6,9 @@
 // (compute_retrieval_metrics: rank of the diagonal in each row of F C^T).
 // SURVEY 8a rows a18/a19, BASELINE cfg 5 (100k x 100k, D = 256).
 //
-// MFMA-bound: three fp32 GEMMs of 2 M N D flops each (exact fp32 products,
-// v_mfma_f32_16x16x4_f32), never materialising S as logits:
+// MFMA-bound: three fp32 GEMMs of 2 M N D flops each (fp32-accurate on the
+// bf16x3 core below, v_mfma_f32_16x16x32_bf16), never materialising S as
+// logits:
 //   k_nce_sim  : S tile = F C^T (K = D) -> E = exp(S/tau - shift) stored in
 //                16x16 MFMA-accumulator tiles (one coalesced 1 KB store per
 //                tile), deterministic row / column partial sums of E, diag.

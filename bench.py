@@ -455,7 +455,7 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    loss = tr.pop_loss_sum() / args.steps
+    loss = tr.pop_loss_sum() / args.steps  # also raises if the peer exchange failed
     pairs = args.steps * B * world
     value = pairs / elapsed
 

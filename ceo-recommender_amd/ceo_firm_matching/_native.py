@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 
 import torch
 
-TT_ABI_VERSION = 1
+TT_ABI_VERSION = 2
 TT_MAX_CAT = 16
 TT_SLOTS_PER_TOWER = 10
 TT_NUM_OFFSETS = 2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER + 1
@@ -118,7 +118,7 @@ def lib() -> ctypes.CDLL:
         "tt_ar_close": (I32, [P]),
         "tt_ar_free": (I32, [P]),
         "tt_ar_reset": (I32, [P, I64, P]),
-        "tt_ar_allreduce_adam": (I32, [ctypes.POINTER(TTArPeers), I32, I32, I64, P, P, P, P, P, H, P, I64, P, P]),
+        "tt_ar_allreduce_adam": (I32, [ctypes.POINTER(TTArPeers), I32, I32, I64, P, P, P, P, P, H, P, I64, P, I64, P]),
         "tt_triplet_workspace_bytes": (I64, [I64, I64, I32]),
         "tt_triplet_forward": (I32, [P, P, I64, I64, I32, I64, F, I64, P, I64, P, P, P, P]),
         "tt_triplet_backward": (I32, [P, P, I64, I64, I32, I64, I64, P, P, P, P, P, P]),

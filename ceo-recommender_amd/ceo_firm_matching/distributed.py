@@ -76,6 +76,7 @@ class PeerExchange:
         for q, r in enumerate(regions):
             self.peers.region[q] = r
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.wait_us = 0  # wait bound per launch (0: the library's 2 s)
         self.epoch = 0  # host epochs of the setup checks (before reset)
         self.timing_us = None  # (exchange, collective) per step, measured by create()
 
@@ -98,15 +99,16 @@ class PeerExchange:
             return None
         if len({h for h, _ in where}) > 1:  # IPC handles do not cross hosts
             return None
+        # agree on reachability BEFORE any mapping collective: a rank that
+        # leaves here early must not strand the others inside _map's gather
         ok = torch.ones(1, dtype=torch.int32, device=flag_dev)
         if not PeerExchange._peers_reachable(where, rank):
             ok.zero_()
-        ex = None
-        if int(ok.item()):
-            try:
-                ex = PeerExchange._map(n, group, device, rank, world)
-            except Exception:  # noqa: BLE001 -- any setup failure keeps the collective
-                ok.zero_()
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if int(ok.item()) == 0:
+            return None
+        ex = PeerExchange._map(n, group, device, rank, world)  # every rank joins its collectives
+        ok.fill_(int(ex is not None))
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # every rank mapped, or none uses it
         if int(ok.item()) == 0:
             if ex is not None:
@@ -139,26 +141,50 @@ class PeerExchange:
             return False
 
     @staticmethod
-    def _map(n, group, device, rank, world):
-        lib = N.lib()
-        nbytes = int(lib.tt_ar_region_bytes(n))
+    def _map(n, group, device, rank, world, lib=None) -> "Optional[PeerExchange]":
+        """Allocate this rank's region and open every peer's.  Always joins
+        the handle all-gather -- a rank whose allocation failed sends a
+        sentinel (status byte 0) -- and returns None after releasing whatever
+        it allocated or opened when any rank could not allocate or this rank
+        could not open a peer's handle."""
+        lib = N.lib() if lib is None else lib
         own = ctypes.c_void_p()
         handle = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)()
-        N.check(lib.tt_ar_alloc(nbytes, ctypes.byref(own), handle), "tt_ar_alloc")
-        mine = torch.tensor(list(bytes(handle)), dtype=torch.uint8)
+        alloc_ok = False
+        try:
+            nbytes = int(lib.tt_ar_region_bytes(n))
+            N.check(lib.tt_ar_alloc(nbytes, ctypes.byref(own), handle), "tt_ar_alloc")
+            alloc_ok = True
+        except Exception:  # noqa: BLE001 -- reported to the peers through the status byte
+            own = ctypes.c_void_p()
+        mine = torch.tensor(list(bytes(handle)) + [int(alloc_ok)], dtype=torch.uint8)
         if dist.get_backend(group) == "nccl":
             mine = mine.to(device)
         allh = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(allh, mine, group=group)
-        regions = []
-        for q in range(world):
-            if q == rank:
-                regions.append(own.value)
-                continue
-            h = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)(*allh[q].cpu().tolist())
-            p = ctypes.c_void_p()
-            N.check(lib.tt_ar_open(h, ctypes.byref(p)), "tt_ar_open")
-            regions.append(p.value)
+        allh = [h.cpu() for h in allh]
+        regions = [None] * world
+        good = all(int(h[-1]) == 1 for h in allh)
+        if good:
+            regions[rank] = own.value
+            for q in range(world):
+                if q == rank:
+                    continue
+                h = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)(*allh[q][:-1].tolist())
+                p = ctypes.c_void_p()
+                try:
+                    N.check(lib.tt_ar_open(h, ctypes.byref(p)), "tt_ar_open")
+                except Exception:  # noqa: BLE001
+                    good = False
+                    break
+                regions[q] = p.value
+        if not good:
+            for q, r in enumerate(regions):
+                if r and q != rank:
+                    lib.tt_ar_close(ctypes.c_void_p(r))
+            if own.value:
+                lib.tt_ar_free(own)
+            return None
         return PeerExchange(lib, regions, own.value, rank, world, n, device)
 
     def close(self):
@@ -184,8 +210,22 @@ class PeerExchange:
         rc = self.lib.tt_ar_allreduce_adam(ctypes.byref(self.peers), self.rank, self.world, self.n,
                                            grad.data_ptr(), ptr(grad_out), ptr(params), ptr(exp_avg),
                                            ptr(exp_avg_sq), hp, ptr(state), int(step_host), self.err.data_ptr(),
-                                           N.stream_ptr(self.device))
+                                           int(self.wait_us), N.stream_ptr(self.device))
         N.check(rc, "tt_ar_allreduce_adam")
+
+    def failed(self) -> bool:
+        """True once any exchange on this rank timed out (reads err: syncs)."""
+        return int(self.err.item()) != 0
+
+    def check(self):
+        """Raise if an exchange timed out.  The device side has already made
+        the failure safe -- a timed-out slice kept its parameters and every
+        later launch on this rank is a no-op -- so the parameters never carry
+        an update computed from the local gradient alone."""
+        if self.failed():
+            raise RuntimeError("peer gradient exchange: a rank did not publish within the wait bound; "
+                               "parameters were left at their last exchanged values "
+                               "(set CEO_TT_PEER_AR=0 to use the RCCL all-reduce)")
 
     def _check(self, group) -> bool:
         g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)

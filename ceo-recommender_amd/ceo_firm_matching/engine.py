@@ -20,7 +20,7 @@ import torch
 
 from . import _native as N
 from .distributed import PeerExchange, average_gradients_, broadcast_state_, world_of
-from .model import CEOFirmMatcher
+from .model import CEOFirmMatcher, check_category_codes
 
 DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")
 
@@ -84,12 +84,7 @@ class FusedTrainer:
             out[k] = t.contiguous()
         g = self.model._geom
         for t, key in enumerate(("firm_cat", "ceo_cat")):
-            counts = g["cat_counts"][t]
-            c = out[key]
-            if counts and c.numel():
-                hi = torch.tensor(counts, device=self.device)
-                if bool(((c[:, :len(counts)] < 0) | (c[:, :len(counts)] >= hi)).any()):
-                    raise IndexError(f"{key}: category code out of range of its embedding table")
+            check_category_codes(out[key], g["cat_counts"][t], key)
         self.data = out
 
     def _batch(self, rows, row0, n_rows, cycle=0, t_base=0):
@@ -116,6 +111,7 @@ class FusedTrainer:
         else:
             self._launch(batch, n_rows, False)
             self.allreduce_and_adam()
+            self._check_eager()
         self.steps_host += 1
 
     def step_cycle(self, rows: torch.Tensor, batch_size: int, n_batches: int, t_base: int = 0):
@@ -128,6 +124,7 @@ class FusedTrainer:
         else:
             self._launch(batch, batch_size, False)
             self.allreduce_and_adam()
+            self._check_eager()
         self.steps_host += 1
 
     def allreduce_and_adam(self):
@@ -142,6 +139,13 @@ class FusedTrainer:
                                     self.state.data_ptr(), 0, N.stream_ptr(self.device))
         N.check(rc, "tt_adam_apply")
 
+    def _check_eager(self):
+        """Eager data-parallel steps on the peer exchange check it every step
+        (a host sync); inside a hipGraph capture the check is the caller's
+        (after each replayed chunk or on the next loss read)."""
+        if self.peer is not None and not torch.cuda.is_current_stream_capturing():
+            self.peer.check()
+
     # ------------------------------------------------------------------ metrics
     def loss_sum_tensor(self) -> torch.Tensor:
         return self.state.view(torch.float32)[4:5]
@@ -151,10 +155,17 @@ class FusedTrainer:
         t = self.loss_sum_tensor()
         v = float(t.item()) if read else None
         t.zero_()
-        if read and self.peer is not None and int(self.peer.err.item()) != 0:
-            raise RuntimeError("peer gradient exchange: a rank did not publish within the wait bound "
-                               "(set CEO_TT_PEER_AR=0 to use the RCCL all-reduce)")
+        if read:
+            self.check_exchange()
         return v
+
+    def check_exchange(self):
+        """Raise if the peer gradient exchange failed (host sync).  Called on
+        every loss read, at the end of train_model and after bench's timed
+        region; between checks a failed rank's launches are device-side no-ops,
+        so its parameters stay at the last exchanged step."""
+        if self.peer is not None:
+            self.peer.check()
 
     def steps_done(self) -> int:
         return int(self.state[0].item())

@@ -94,3 +94,11 @@ def explain_model_pdp(wrapper: ModelWrapper, df: pd.DataFrame, features_to_plot:
     print(f"Saved PDP plots to {path}")
     plt.close(fig)
     return curves
+
+
+def explain_model_shap(wrapper: ModelWrapper, df: pd.DataFrame):
+    """Reference explain.py:134-170 (SHAP KernelExplainer summary plot).
+    Not part of this build: the ``shap`` package is absent from the image and
+    the explainer is off the training path (the reference CLI disables it)."""
+    raise NotImplementedError("explain_model_shap needs the 'shap' package, which this MI355X build does not "
+                              "ship; use explain_model_pdp (batched on the fused eval forward)")

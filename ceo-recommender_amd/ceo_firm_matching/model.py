@@ -309,6 +309,19 @@ class _FusedTowerEmbeddings(torch.autograd.Function):
 
 
 
+def check_category_codes(cat: Optional[torch.Tensor], counts, what: str):
+    """Raise IndexError when a categorical code is outside its embedding table,
+    as the reference's nn.Embedding does (model.py:69,74); the fused kernels
+    would otherwise clamp it.  One reduction + host read per call, and only
+    for towers that have categorical columns."""
+    if not counts or cat is None or cat.numel() == 0:
+        return
+    k = len(counts)
+    hi = torch.tensor(counts, device=cat.device, dtype=cat.dtype)
+    if bool(((cat[:, :k] < 0) | (cat[:, :k] >= hi)).any()):
+        raise IndexError(f"{what}: category code out of range of its embedding table")
+
+
 def _fused_inputs(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
     dev = f_numeric.device
     if model.logit_scale.device != dev:
@@ -326,6 +339,8 @@ def _fused_inputs(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
             raise RuntimeError(f"tower {TOWERS[t]}: expected [B, {len(g['cat_counts'][t])}] categorical input")
     if f_num.shape[0] != c_num.shape[0]:
         raise RuntimeError("firm and CEO batches differ in size")
+    check_category_codes(f_cat, g["cat_counts"][0], "firm_cat")
+    check_category_codes(c_cat, g["cat_counts"][1], "ceo_cat")
     params = [p for _, p, _ in model._named_slots(N.param_offsets(model._arena.desc))]
     return f_num, f_cat, c_num, c_cat, params
 

@@ -72,6 +72,23 @@ def generate_synthetic_data(n_samples: int = 1000) -> pd.DataFrame:
     return pd.DataFrame(data)
 
 
+def generate_structural_synthetic_data(n_samples: int = 2000, seed: int = 42) -> pd.DataFrame:
+    """Reference synthetic.py:78-110: the base frame plus BLM posterior type
+    probabilities ``prob_ceo_1..5`` / ``prob_firm_1..5`` (flat Dirichlet, drawn
+    from the global numpy RNG after the base frame's draws, which reseed 42)
+    and ``tenure`` = (fiscalyear - ceo_year) clipped at 0."""
+    np.random.seed(seed)
+    df = generate_synthetic_data(n_samples)
+    ceo = np.random.dirichlet(np.ones(5), n_samples)
+    for i in range(5):
+        df[f'prob_ceo_{i + 1}'] = ceo[:, i]
+    firm = np.random.dirichlet(np.ones(5), n_samples)
+    for i in range(5):
+        df[f'prob_firm_{i + 1}'] = firm[:, i]
+    df['tenure'] = (df['fiscalyear'] - df['ceo_year']).clip(lower=0)
+    return df
+
+
 def generate_pairs(n: int, n_firm: int, n_ceo: int, seed: int = 42,
                    device: Optional[torch.device] = None, chunk: int = 1 << 22) -> Dict[str, torch.Tensor]:
     """Scaled (firm, CEO) pair dataset in the CEOFirmDataset dict layout."""

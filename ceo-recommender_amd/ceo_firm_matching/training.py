@@ -89,6 +89,7 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> C
             print(f"Epoch {epoch}: Avg Train Loss = {avg_loss:.4f}")
         else:
             trainer.pop_loss_sum(read=False)
+    trainer.check_exchange()
     model._trainer = trainer  # keeps optimizer state reachable for callers/tests
     return model
 

@@ -1035,7 +1035,7 @@ int32_t tt_ar_reset(void* region, int64_t n, tt_stream_t stream) {
 int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t world, int64_t n, const float* grad,
                              float* grad_out, float* params, float* exp_avg, float* exp_avg_sq,
                              const tt_adam_hp* hp, tt_state* state, int64_t step_host, int32_t* err,
-                             tt_stream_t stream) {
+                             int64_t wait_us, tt_stream_t stream) {
   if (!peers || world < 1 || world > TT_AR_MAX_RANKS || rank < 0 || rank >= world || n < 1 || !grad || !err)
     return TT_ERR_ARG;
   if (params && (!exp_avg || !exp_avg_sq || !hp)) return TT_ERR_ARG;
@@ -1067,7 +1067,8 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
   a.state = state;
   a.step_host = step_host;
   a.err = err;
-  a.wait_ticks = 200000000ull;  // 2 s of polling, then give up (err)
+  // s_memrealtime runs at 100 MHz; default bound 2 s of polling, then give up (err)
+  a.wait_ticks = (uint64_t)(wait_us > 0 ? wait_us : 2000000) * 100ull;
   hipLaunchKernelGGL(k_ar_adam, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
   return launch_check();
 }

@@ -20,8 +20,13 @@
 //   wrote after finishing its step-t reads (stream order).
 //   The epoch is the device step counter (tt_state.step_cur), so the launch
 //   replays unchanged inside a captured hipGraph.
-//   A wait that exceeds its bound sets *err and gives up (no hang); the host
-//   checks err and falls back to RCCL.
+//   A wait that exceeds its bound sets *err and gives up (no hang).  The
+//   failure is never papered over with local data: a block that timed out
+//   leaves its slice of p / m / v / grad_out untouched, and every later launch
+//   on this rank sees *err != 0 at entry and does nothing at all -- it neither
+//   applies Adam nor publishes, so the peers time out in turn and stop
+//   updating too, and no slot is rewritten while a slow peer may still read
+//   it.  The host checks err (FusedTrainer.check_exchange) and raises.
 #include "tt_common.h"
 
 namespace tt {
@@ -49,6 +54,12 @@ __device__ __forceinline__ uint64_t ld_flag(const uint64_t* f) {
 }
 
 __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
+  // sticky failure: an earlier exchange on this rank timed out (one read per
+  // block, so the whole block takes the same branch)
+  __shared__ int ok_s;
+  if (threadIdx.x == 0) ok_s = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  __syncthreads();
+  if (ok_s == 0) return;
   const int64_t t = a.state ? a.state->step_cur : a.step_host;
   const uint64_t epoch = (uint64_t)t;
   const int b = blockIdx.x;
@@ -74,9 +85,6 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
     __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 3. wait for every rank's slice b (bounded)
-  __shared__ int ok_s;
-  if (threadIdx.x == 0) ok_s = 1;
-  __syncthreads();
   if (threadIdx.x < a.world) {
     const uint64_t* f = a.flags[a.rank] + (int64_t)threadIdx.x * a.blocks + b;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz, chip-wide
@@ -90,19 +98,15 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
     }
   }
   __syncthreads();
-  const bool ok = ok_s != 0;
+  if (ok_s == 0) return;  // this slice keeps its parameters (err reports it)
   // 4. mean over ranks in rank order + Adam
   const float inv_w = 1.0f / (float)a.world;
   AdamCoef c;
   if (a.p) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
   for (int64_t e = lo + threadIdx.x; e < hi; e += AR_THREADS) {
     float s = 0.f;
-    if (ok) {
-      for (int q = 0; q < a.world; ++q)
-        s += __hip_atomic_load(a.slot[q] + par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-      s = a.grad[e] * (float)a.world;  // timed out: local gradient (err reports it)
-    }
+    for (int q = 0; q < a.world; ++q)
+      s += __hip_atomic_load(a.slot[q] + par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const float g = s * inv_w;
     if (a.grad_out) a.grad_out[e] = g;
     if (a.p) {

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TT_ABI_VERSION 1
+#define TT_ABI_VERSION 2
 #define TT_MAX_CAT 16      /* categorical columns per tower */
 
 /* status codes */
@@ -256,8 +256,12 @@ int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n
  * points allocate / map memory (unlike the compute entries); the caller
  * exchanges the TT_AR_HANDLE_BYTES handles between ranks (e.g. an all-gather)
  * and passes every rank's mapped region in tt_ar_peers.  A wait that exceeds
- * its bound increments *err instead of hanging (the result is then the local
- * gradient); the caller checks err and falls back to its collective.      */
+ * its bound (wait_us; <= 0: 2 s) increments *err instead of hanging: that
+ * block's slice of params / exp_avg / exp_avg_sq / grad_out is left
+ * untouched, and every later call with *err != 0 returns on the device
+ * without publishing or updating anything (the peers then time out too).
+ * The caller checks *err and fails the step; *err is cleared only by
+ * re-creating the exchange (tt_ar_reset on every rank).                   */
 #define TT_AR_MAX_RANKS 16
 #define TT_AR_HANDLE_BYTES 64
 typedef struct tt_ar_peers {
@@ -277,7 +281,7 @@ int32_t tt_ar_reset(void* region, int64_t n, tt_stream_t stream);
 int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t world, int64_t n,
                              const float* grad, float* grad_out, float* params, float* exp_avg,
                              float* exp_avg_sq, const tt_adam_hp* hp, tt_state* state,
-                             int64_t step_host, int32_t* err, tt_stream_t stream);
+                             int64_t step_host, int32_t* err, int64_t wait_us, tt_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -466,7 +466,25 @@ def gen_contrastive_train():
     print("wrote contrastive_train.npz:", list(out["nce/printed"]), list(out["tri/printed"]))
 
 
+def gen_synthetic():
+    """``synthetic.npz``: numeric columns of generate_synthetic_data(300) and
+    generate_structural_synthetic_data(300, seed=7) (synthetic.py:10-110)."""
+    from ceo_firm_matching.synthetic import generate_structural_synthetic_data, generate_synthetic_data
+    out = {}
+    base = generate_synthetic_data(300)
+    for k in ("gvkey", "Age", "maxedu", "ind_firms_60w", "logatw", "match_means", "sd_match_means", "fiscalyear"):
+        out[f"base/{k}"] = base[k].to_numpy()
+    out["base/compindustry"] = base["compindustry"].to_numpy().astype("U8")
+    st = generate_structural_synthetic_data(300, seed=7)
+    for k in [f"prob_ceo_{i}" for i in range(1, 6)] + [f"prob_firm_{i}" for i in range(1, 6)] + ["tenure"]:
+        out[f"structural/{k}"] = st[k].to_numpy()
+    np.savez_compressed(os.path.join(HERE, "synthetic.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["synthetic"]:
+        gen_synthetic()
+        sys.exit(0)
     if sys.argv[1:] == ["contrastive_train"]:
         gen_contrastive_train()
         sys.exit(0)
@@ -483,3 +501,4 @@ if __name__ == "__main__":
     gen_contrastive()
     gen_triplet()
     gen_contrastive_train()
+    gen_synthetic()

@@ -248,7 +248,7 @@ def test_embedding_mining_exchange_host_argument_errors():
         peers.region[q] = p
     hp = N.adam_hp(4e-4)
     run = lambda rank, world, n, err, params=None, step=1: L.tt_ar_allreduce_adam(  # noqa: E731
-        ctypes.byref(peers), rank, world, n, p, p, params, p, p, ctypes.byref(hp), None, step, err, None)
+        ctypes.byref(peers), rank, world, n, p, p, params, p, p, ctypes.byref(hp), None, step, err, 0, None)
     assert run(0, 0, 100, p) == N.TT_ERR_ARG
     assert run(2, 2, 100, p) == N.TT_ERR_ARG
     assert run(0, N.TT_AR_MAX_RANKS + 1, 100, p) == N.TT_ERR_ARG

@@ -134,3 +134,66 @@ def test_data_parallel_step_on_peer_exchange(world):
         pytest.skip("no HIP device")
     for rank, err, where in _spawn(_ddp_peer_rank, world):
         assert err < 1e-5, (rank, err, where)
+
+
+def test_exchange_timeout_leaves_parameters_and_raises():
+    """A peer that never launches: the waiting rank's exchange times out,
+    leaves params / exp_avg / exp_avg_sq / grad_out untouched (never the local
+    gradient), every later launch is a device-side no-op that publishes
+    nothing, and the host check raises.  One process owns both regions (the
+    second rank simply never runs)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ctypes
+    from ceo_firm_matching import _native as N
+    from ceo_firm_matching.distributed import PeerExchange
+    L = N.lib()
+    dev = torch.device("cuda:0")
+    n = 5000
+    nbytes = int(L.tt_ar_region_bytes(n))
+    regs = []
+    for _ in range(2):
+        r = ctypes.c_void_p()
+        h = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)()
+        N.check(L.tt_ar_alloc(nbytes, ctypes.byref(r), h), "tt_ar_alloc")
+        regs.append(r.value)
+    ex = PeerExchange(L, regs, regs[0], 0, 2, n, dev)
+    ex.regions = [regs[0], None]  # close() must not IPC-close the second (local) region
+    ex.wait_us = 20_000
+    try:
+        g = torch.Generator(device=dev).manual_seed(3)
+        p = torch.randn(n, device=dev, generator=g)
+        m = torch.randn(n, device=dev, generator=g).abs()
+        v = torch.randn(n, device=dev, generator=g).abs()
+        x = torch.randn(n, device=dev, generator=g)
+        out = torch.full((n,), 7.0, device=dev)
+        p0, m0, v0 = p.clone(), m.clone(), v.clone()
+        hp = N.adam_hp(4e-4)
+        ex.run(x, grad_out=out, params=p, exp_avg=m, exp_avg_sq=v, hp=hp, step_host=1)
+        torch.cuda.synchronize()
+        assert ex.failed()
+        assert torch.equal(p, p0) and torch.equal(m, m0) and torch.equal(v, v0)
+        assert bool((out == 7.0).all())
+        # the peer's flag array holds rank 0's step-1 flags (published before the wait)
+        flags1 = torch.empty(N.TT_AR_MAX_RANKS * 32, dtype=torch.int64, device=dev)
+        hip = ctypes.CDLL("libamdhip64.so")
+        assert hip.hipMemcpy(ctypes.c_void_p(flags1.data_ptr()), ctypes.c_void_p(regs[1]),
+                             ctypes.c_size_t(flags1.numel() * 8), 3) == 0  # device to device
+        torch.cuda.synchronize()
+        assert bool((flags1[:32] == 1).all())
+        err_before = int(ex.err.item())
+        # sticky: step 2 neither waits, nor publishes, nor updates
+        ex.run(x, grad_out=out, params=p, exp_avg=m, exp_avg_sq=v, hp=hp, step_host=2)
+        torch.cuda.synchronize()
+        assert int(ex.err.item()) == err_before
+        assert torch.equal(p, p0) and bool((out == 7.0).all())
+        assert hip.hipMemcpy(ctypes.c_void_p(flags1.data_ptr()), ctypes.c_void_p(regs[1]),
+                             ctypes.c_size_t(flags1.numel() * 8), 3) == 0
+        torch.cuda.synchronize()
+        assert bool((flags1[:32] == 1).all())
+        with pytest.raises(RuntimeError, match="did not publish"):
+            ex.check()
+    finally:
+        torch.cuda.synchronize()
+        L.tt_ar_free(ctypes.c_void_p(regs[1]))
+        ex.close()

@@ -149,3 +149,26 @@ def test_interaction_grid_on_fused_eval_forward():
     got = [interaction_grid(model, proc, xf, yf)[2] for xf, yf in (("logatw", "Age"), ("maxedu", "rdintw"))]
     for g_, r_ in zip(got, ref):
         assert normwise(g_, r_) < 1e-5
+
+
+def test_out_of_range_category_code_raises_index_error():
+    """model(...) on the fused path raises IndexError for a code outside its
+    embedding table, as the reference's nn.Embedding does (model.py:69,74),
+    instead of the kernels' clamped gather; in-range codes still run."""
+    _need_gpu()
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    dev = torch.device("cuda:0")
+    meta = {"n_firm_numeric": 12, "firm_cat_counts": [4, 4, 2, 2],
+            "n_ceo_numeric": 2, "ceo_cat_counts": [2, 4, 2, 2, 2, 2, 2]}
+    torch.manual_seed(0)
+    m = CEOFirmMatcher(meta, Config()).to(dev).eval()
+    B = 16
+    fn, cn = torch.randn(B, 12, device=dev), torch.randn(B, 2, device=dev)
+    fc = torch.zeros(B, 4, dtype=torch.int64, device=dev)
+    cc = torch.zeros(B, 7, dtype=torch.int64, device=dev)
+    assert m(fn, fc, cn, cc).shape == (B, 1)
+    for bad, which in ((4, "firm"), (-1, "firm"), (2, "ceo")):
+        f2, c2 = fc.clone(), cc.clone()
+        (f2 if which == "firm" else c2)[3, 1 if which == "firm" else 0] = bad
+        with pytest.raises(IndexError):
+            m(fn, f2, cn, c2)

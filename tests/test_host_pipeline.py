@@ -135,3 +135,33 @@ def test_peer_exchange_reachability_rule():
     assert PeerExchange._peers_reachable(same, 0) and PeerExchange._peers_reachable(same, 1)
     if not torch.cuda.is_available():
         assert not PeerExchange._peers_reachable([("h", 0), ("h", 1)], 0)
+
+
+def test_synthetic_generators_match_reference_fixture():
+    """generate_synthetic_data / generate_structural_synthetic_data draw the
+    reference's values (tests/golden/synthetic.npz, made by importing the
+    reference: synthetic.py:10-110)."""
+    from ceo_firm_matching import generate_structural_synthetic_data
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "synthetic.npz"))
+    base = generate_synthetic_data(300)
+    st = generate_structural_synthetic_data(300, seed=7)
+    for key in g.files:
+        part, col = key.split("/")
+        got = (base if part == "base" else st)[col].to_numpy()
+        if got.dtype.kind in "OU":
+            assert list(got.astype(str)) == list(g[key].astype(str)), key
+        else:
+            np.testing.assert_array_equal(got, g[key], err_msg=key)
+    probs = st[[f"prob_ceo_{i}" for i in range(1, 6)]].to_numpy().sum(1)
+    np.testing.assert_allclose(probs, 1.0, rtol=1e-12)
+
+
+def test_reference_top_level_names_importable():
+    """The reference's two-tower top-level names (reference __init__.py:7-13)."""
+    import ceo_firm_matching as P
+    for name in ("Config", "DataProcessor", "CEOFirmDataset", "CEOFirmMatcher", "train_model", "ModelWrapper",
+                 "explain_model_pdp", "explain_model_shap", "plot_interaction_heatmap",
+                 "generate_synthetic_data", "generate_structural_synthetic_data", "contrastive"):
+        assert hasattr(P, name), name
+    with pytest.raises(NotImplementedError):
+        P.explain_model_shap(None, None)

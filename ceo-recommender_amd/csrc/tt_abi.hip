@@ -38,6 +38,7 @@ struct Layout {
   int64_t n;          // parameter count
   int64_t so[2][6];   // slab offsets W0 b0 W4 b4 W8 b8
   int64_t slab_ld;
+  bool fold;          // numeric-only towers, kp <= 64: BN0 backward folded into k_bwd_mid
 };
 
 static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
@@ -67,10 +68,18 @@ static Layout make_layout(const tt_model_desc* d) {
       off = round_up(off + (int64_t)d->cat_counts[t][j] * d->emb_dim[t], 4);
     }
   const int D = d->latent;
+  L.fold = true;
   for (int t = 0; t < 2; ++t) {
     const int in = d->n_num[t] + d->n_cat[t] * d->emb_dim[t];
     L.in_dim[t] = in;
     L.kp[t] = (int)round_up(in, 16);
+    L.fold = L.fold && d->n_cat[t] == 0 && in % 4 == 0 && L.kp[t] <= FOLD_MAX_KP;
+  }
+#ifdef TT_NO_FOLD
+  L.fold = false;
+#endif
+  for (int t = 0; t < 2; ++t) {
+    const int in = L.in_dim[t];
     const int64_t sz[TT_SLOTS_PER_TOWER] = {(int64_t)H0 * in, H0, H0, H0, (int64_t)H1 * H0, H1, H1, H1,
                                             (int64_t)D * H1, D};
     for (int s = 0; s < TT_SLOTS_PER_TOWER; ++s) {
@@ -78,7 +87,8 @@ static Layout make_layout(const tt_model_desc* d) {
       off = round_up(off + sz[s], 4);
     }
     int64_t so = 0;
-    L.so[t][0] = so; so += (int64_t)H0 * in;
+    // folded: P and Q partials interleaved [64][kp/16][P 16 | Q 16] in the W0 range
+    L.so[t][0] = so; so += (int64_t)H0 * (L.fold ? 2 * L.kp[t] : in);
     L.so[t][1] = so; so += H0;
     L.so[t][2] = so; so += (int64_t)H1 * H0;
     L.so[t][3] = so; so += H1;
@@ -93,6 +103,7 @@ static Layout make_layout(const tt_model_desc* d) {
 
 struct WsLayout {
   int64_t Z0[2], Z4[2], dY0[2], dY1[2], st0[2], st1[2], sh0[2], sh1[2], fin0[2], fin1[2], bng[2], lsr;
+  int64_t fr, k0s[2], xsh[2];  // folded BN0 backward: replicas (both towers), inv0*gamma0, shift row
   int64_t tgw;
   int64_t slab[2];
   int64_t gacc;
@@ -123,6 +134,11 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
     W.fin1[t] = take(2 * H1);
   }
   W.lsr = take(NREP * LSR);
+  W.fr = take(2 * NREP * FRW);
+  for (int t = 0; t < 2; ++t) {
+    W.k0s[t] = take(H0);
+    W.xsh[t] = take(FOLD_MAX_KP);
+  }
   W.gacc = take(L.n);
   const int64_t rows = padded_rows(max_batch);
   W.n_tiles = (int)(rows / ROWS);
@@ -154,7 +170,8 @@ static void set_lds_attrs() {
                         (const void*)k_top<4, 128, false>, (const void*)k_top<8, 128, false>,
                         (const void*)k_top<4, 64, true>,  (const void*)k_top<8, 64, true>,
                         (const void*)k_top<4, 128, true>, (const void*)k_top<8, 128, true>,
-                        (const void*)k_bwd_mid<ROWS>,    (const void*)k_bwd_first<ROWS>};
+                        (const void*)k_bwd_mid<ROWS>, (const void*)k_bwd_mid_fold<FOLD_ROWS, true>,
+                        (const void*)k_bwd_mid_fold<FOLD_ROWS, false>, (const void*)k_bwd_first<ROWS>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   });
 }
@@ -165,6 +182,7 @@ struct Plan {
   int top_rows;     // row tile of k_top (64, or 128 for large batches)
   int n_tiles;      // 64-row tiles
   int n_tiles_top;  // k_top tiles
+  int n_tiles_mid;  // k_bwd_mid tiles (FOLD_ROWS rows when the BN0 backward is folded)
 };
 
 static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P) {
@@ -183,12 +201,13 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   // kernel reads was written earlier in the same step
   P->n_tiles = (int)(padded_rows(B) / ROWS);
   P->n_tiles_top = (int)((P->n_tiles * ROWS) / P->top_rows);
+  P->n_tiles_mid = L.fold ? (int)((P->n_tiles * ROWS) / FOLD_ROWS) : P->n_tiles;
   P->lds_l0 = L0Lds<ROWS>::bytes(kpm);
   P->lds_l4 = L4Lds<ROWS>::bytes;
   const int tl = P->ndt == 4 ? (P->top_rows == 64 ? TopLds<4, 64>::total : TopLds<4, 128>::total)
                              : (P->top_rows == 64 ? TopLds<8, 64>::total : TopLds<8, 128>::total);
   P->lds_top = sizeof(float) * (size_t)tl;
-  P->lds_mid = MidLds<ROWS>::bytes;
+  P->lds_mid = L.fold ? FoldLds<FOLD_ROWS>::bytes : MidLds<ROWS>::bytes;
   P->lds_first = FirstLds<ROWS>::bytes(kpm);
   (void)emb;
   for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first})
@@ -271,6 +290,17 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
     T.so_b4 = L.so[t][3];
     T.so_W8 = L.so[t][4];
     T.so_b8 = L.so[t][5];
+    T.fr = ws + W.fr + (int64_t)t * NREP * FRW;
+    T.k0s = ws + W.k0s[t];
+    T.xsh = ws + W.xsh[t];
+    if (L.fold) {  // the folded k_bwd_mid accumulates gg0 | gbe0 into the fold replicas
+      T.gg0 = T.fr;
+      T.gbe0 = T.fr + H0;
+    }
+  }
+  if (L.fold) {
+    a.fr_zero = ws + W.fr;
+    a.fr_zero_len = 2 * NREP * FRW;
   }
   a.target = b->target;
   a.weight = b->weight;
@@ -319,13 +349,38 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     const int64_t* s = L.slot[t];
     float* bng = ws + W.bng[t];
     // gamma|beta slots are adjacent and unpadded (H0, H1 multiples of 4): same order as a replica
-    add(s[TT_SLOT_W0], s[TT_SLOT_G0] - s[TT_SLOT_W0], 0, t, L.so[t][0], P.n_tiles);
-    add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, bng, BNG);
-    add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles);
+    if (L.fold) {
+      float* fr = ws + W.fr + (int64_t)t * NREP * FRW;
+      for (int kind = 3; kind <= 4; ++kind) {
+        add(s[kind == 3 ? TT_SLOT_W0 : TT_SLOT_B0], kind == 3 ? (int64_t)H0 * L.in_dim[t] : H0, kind, t,
+            L.so[t][0], P.n_tiles_mid, fr, FRW);
+        Seg& g = r.seg[k - 1];
+        g.in = L.in_dim[t];
+        g.kp = L.kp[t];
+        g.k0 = ws + W.k0s[t];
+        g.xsh = ws + W.xsh[t];
+      }
+      add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, fr, FRW);
+      r.seg[k - 1].keep = 1;  // zeroed by the next step's k_l0_fwd
+    } else {
+      add(s[TT_SLOT_W0], s[TT_SLOT_G0] - s[TT_SLOT_W0], 0, t, L.so[t][0], P.n_tiles);
+      add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, bng, BNG);
+    }
+    add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles_mid);
     add(s[TT_SLOT_G1], 2 * H1, 2, t, 0, 0, bng + 2 * H0, BNG);
     add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], 0, t, L.so[t][4], P.n_tiles_top);
   }
   add(L.ls, 1, 2, 0, 0, 0, ws + W.lsr, LSR);
+  // element space of k_reduce_adam: every range starts on a block (one
+  // segment per block); kind 3 ranges hold every W0 element twice (P and Q
+  // halves of one 32-lane group)
+  int64_t vo = 0;
+  for (int i = 0; i < k; ++i) {
+    r.seg[i].voff = vo;
+    r.seg[i].vlen = r.seg[i].kind == 3 ? 2 * r.seg[i].len : r.seg[i].len;
+    vo = round_up(vo + r.seg[i].vlen, RED_E);
+  }
+  r.vn = vo;
   r.lsr = ws + W.lsr;
   r.n_seg = k;
   r.n_slabs = P.n_tiles;
@@ -401,11 +456,31 @@ static void launch_l4(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = 
   launch(k_l4_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l4, s, ev, a);
 }
 static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
-  launch(k_bwd_mid<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_mid, s, ev, a);
+  if (!a.fr_zero) {
+    launch(k_bwd_mid<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_mid, s, ev, a);
+    return;
+  }
+  const dim3 grid(P.n_tiles_mid, 2), blk(4 * FOLD_ROWS);
+  if (a.tw[0].num_vec && a.tw[1].num_vec)
+    launch(k_bwd_mid_fold<FOLD_ROWS, true>, grid, blk, P.lds_mid, s, ev, a);
+  else
+    launch(k_bwd_mid_fold<FOLD_ROWS, false>, grid, blk, P.lds_mid, s, ev, a);
 }
+// folded BN0 backward: nothing to launch (the events, when given, bracket nothing)
 static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
+  if (a.fr_zero) {
+    if (ev.e0 && ev.e1) {
+      (void)hipEventRecord(ev.e0, s);
+      (void)hipEventRecord(ev.e1, s);
+    }
+    return;
+  }
   launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
+static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}) {
+  launch(k_reduce_adam, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
+}
+
 template <bool EMB>
 static void launch_top_t(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev) {
   const dim3 grid(P.n_tiles_top, grid_y), blk(4 * P.top_rows);
@@ -527,12 +602,13 @@ static int32_t backward_impl(const tt_model_desc* d, const float* params, const 
   (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
   for (int t = 0; t < 2; ++t) (void)hipMemsetAsync(w + c.W.bng[t], 0, sizeof(float) * NREP * BNG, s);
   (void)hipMemsetAsync(w + c.W.lsr, 0, sizeof(float) * NREP * LSR, s);
+  if (c.L.fold) (void)hipMemsetAsync(w + c.W.fr, 0, sizeof(float) * 2 * NREP * FRW, s);
   launch_top(a, c.P, 2, s);
   launch_mid(a, c.P, s);
   launch_first(a, c.P, s);
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
-  const int nb = (int)((c.L.n + RED_E - 1) / RED_E);
-  hipLaunchKernelGGL(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, r);
+  r.inv_b = 1.f / (float)b->n_rows;
+  launch_reduce(r, s);
   return launch_check();
 }
 
@@ -581,6 +657,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   launch_mid(a, c.P, s, ev(3));
   launch_first(a, c.P, s, ev(4));
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
+  r.inv_b = 1.f / (float)b->n_rows;
   for (int t = 0; t < 2; ++t) {
     r.zero_buf[2 * t] = w + c.W.st0[t];
     r.zero_len[2 * t] = NREP * 2 * H0;
@@ -599,8 +676,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     r.eps = hp->eps;
     r.state = state;
   }
-  const int nb = (int)((c.L.n + RED_E - 1) / RED_E);
-  launch(k_reduce_adam, dim3(nb), dim3(RED_E * RED_G), 0, s, ev(5), r);
+  launch_reduce(r, s, ev(5));
   return launch_check();
 }
 

@@ -25,6 +25,11 @@ constexpr int MAX_KP = 256;  // padded tower input width supported by the fused 
 // the consumers sum NREP values.
 constexpr int NREP = 16;
 constexpr int BNG = 2 * H0 + 2 * H1;  // one replica of a tower's BN-affine grads: gg0|gbe0|gg1|gbe1
+// Folded BN0 backward (k_bwd_mid<R, true>, numeric-only towers with kp <= 64):
+// one replica of a tower's fold sums: gg0 | gbe0 | sum Zhat0 | sum (X - shift)
+constexpr int FRW = 3 * H0 + 64;
+constexpr int FOLD_MAX_KP = 64;
+constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 constexpr int LSR = 32;               // replica stride of the (dls, loss) pair
 __device__ __forceinline__ int rep_of_block() { return (int)(blockIdx.x % NREP); }
 
@@ -330,6 +335,8 @@ struct TowerDev {
   float *fin0, *fin1;                     // finalized mean|invstd [2*64], [2*32]
   float* slab;                            // [n_slabs][slab_ld] partial dW/db sums
   int64_t so_W0, so_b0, so_W4, so_b4, so_W8, so_b8;  // offsets inside one slab
+  float* fr;                              // folded: [NREP][FRW] replicas (zeroed by k_l0_fwd)
+  float *k0s, *xsh;                       // folded: inv0*gamma0 [64], shift row [64] (block 0 writes)
 };
 
 enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2, TOP_EMB_FWD = 3, TOP_EMB_BWD = 4 };
@@ -360,6 +367,8 @@ struct StepArgs {
   float* tgw;            // [Bpad][2] (target, weight) of each batch row, gathered by k_l0_fwd
   float* emb;            // [2][B][D] raw tower outputs U | V (TOP_EMB_FWD)
   const float* demb;     // [2][B][D] upstream dU | dV (TOP_EMB_BWD)
+  float* fr_zero;        // k_l0_fwd zeroes fr_zero[0, fr_zero_len) (both towers' fold replicas)
+  int fr_zero_len;
 };
 
 // ---------------------------------------------------------------------------
@@ -565,24 +574,23 @@ __device__ __forceinline__ float tower_x(const TowerDev& T, int64_t drow, int co
 // ---------------------------------------------------------------------------
 constexpr int MAX_SEG = 48;
 #ifndef TT_RED_MINW
-#define TT_RED_MINW 8  // waves per SIMD: <= 64 VGPRs, 4 blocks of 512 per CU (every block resident); 8.50 -> 8.25 us
+#define TT_RED_MINW 7  // waves per SIMD: <= 73 VGPRs (no spills with 16 loads in flight); 9.4 us vs 10.8 at 8
 #endif
-#ifndef TT_RED_E
-#define TT_RED_E 32
-#endif
-#ifndef TT_RED_G
-#define TT_RED_G 16  // 512 threads, 16 slab loads each (A/B over 4x4..64x16 shapes, tools/gpu_bench_multi.sh)
-#endif
-constexpr int RED_E = TT_RED_E;   // elements per block
-constexpr int RED_G = TT_RED_G;   // slab groups per element
+constexpr int RED_E = 32;  // elements per k_reduce_adam block
+constexpr int RED_G = 16;  // slab groups per element (512 threads, 16 slab loads each)
 
 struct Seg {
   int64_t off, len;      // range in the parameter arena
+  int64_t voff, vlen;    // range in k_reduce_adam's element space (kind 3: 2 len, 32-aligned)
   int64_t slab_off;      // offset of the range inside a tower slab (kind 0)
-  int32_t kind, tower;   // kind 0: slab partials, 1: atomic accumulator (gacc), 2: NREP replicas
-  int32_t n_slabs, pad;  // partial slabs to sum (kind 0)
-  float* rep;            // kind 2: replica 0 of the range; replica r at + r * rep_stride
+  // kind 0: slab partials, 1: atomic accumulator (gacc), 2: NREP replicas,
+  // 3: W0 of the folded BN0 backward, 4: b0 of the folded BN0 backward
+  int32_t kind, tower;
+  int32_t n_slabs, keep; // partial slabs to sum (kinds 0, 3); keep: kind 2 leaves its replicas (no zeroing)
+  float* rep;            // kinds 2-4: replica 0 of the range; replica r at + r * rep_stride
   int64_t rep_stride;
+  int32_t in, kp;        // kinds 3, 4: tower input width, padded width (P|Q rows: 2 kp floats)
+  const float *k0, *xsh; // kinds 3, 4: inv0*gamma0, shift row
 };
 
 struct RedArgs {
@@ -590,6 +598,7 @@ struct RedArgs {
   int32_t n_seg;
   int32_t n_slabs;
   int64_t n;
+  int64_t vn;            // k_reduce_adam elements (blocks = vn / RED_E)
   const float* slab[2];
   int64_t slab_ld;
   float* gacc;
@@ -603,6 +612,7 @@ struct RedArgs {
   float lr, b1, b2, eps;
   tt_state* state;
   int64_t step_host;
+  float inv_b;           // 1 / batch rows (kinds 3, 4)
 };
 
 }  // namespace tt

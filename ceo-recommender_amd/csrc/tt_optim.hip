@@ -39,21 +39,43 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   p = p + (-c.step_size) * (m / denom);
 }
 
+// Element space: block b, lane (pg, el) takes virtual element v = b RED_E + el.
+// Every segment's virtual range starts on a block boundary, so the segment
+// (and its kind) is uniform per block: one scalar lookup, no per-lane
+// divergence.  Ranges map one to one onto the parameter arena, except kind 3
+// (W0 of the folded BN0 backward, slab partials laid out [64][kp/16][P 16 |
+// Q 16]): each 32-element group of its range covers 16 W0 elements twice --
+// el < 16 sums their P partials, el >= 16 the Q partials of the same
+// elements -- so the owner finds both sums in this block's LDS and every lane
+// reads 64 B of one 128-B P|Q row segment.
 __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedArgs a) {
+  static_assert(RED_G == NREP, "kinds 3, 4: group pg takes replica pg");
+  static_assert(RED_E == 32, "kind 3 pairs lanes el and el + 16");
   __shared__ float part[RED_G][RED_E];
+  __shared__ float xpart[4][RED_G][RED_E];  // kinds 3, 4: gg0, gbe0, sum Zh0, sum X' replicas
   TT_STAMP(5, 0);
   // the step first: a later load would make its wait (in-order vmcnt) wait for the slabs
   const int64_t t = a.state ? a.state->step_cur : a.step_host;
   const int el = threadIdx.x & (RED_E - 1), pg = threadIdx.x / RED_E;
-  const int64_t e = (int64_t)blockIdx.x * RED_E + el;
+  const int64_t vb = (int64_t)blockIdx.x * RED_E;
   int si = -1;
-  if (e < a.n)
-    for (int k = 0; k < a.n_seg; ++k)
-      if (e >= a.seg[k].off && e < a.seg[k].off + a.seg[k].len) { si = k; break; }
+  for (int k = 0; k < a.n_seg; ++k)
+    if (vb >= a.seg[k].voff && vb < a.seg[k].voff + a.seg[k].vlen) { si = k; break; }
+  si = __builtin_amdgcn_readfirstlane(si);
+  if (si < 0) return;  // padding between ranges (whole block)
+  const Seg& S = a.seg[si];
+  const int kind = S.kind;
+  const int64_t dv = vb + el - S.voff;
+  const bool live = dv < S.vlen;
+  // parameter element of this lane; kind 3: W0 element and which half (P / Q)
+  const bool qhalf = kind == 3 && (el & 16) != 0;
+  const int wi = kind == 3 ? (int)(dv >> 5) * 16 + (el & 15) : 0;
+  const int64_t e = S.off + (kind == 3 ? (int64_t)wi : dv);
   // the Adam state of this element is loaded up front: its latency overlaps the slab loads
-  const bool owner = pg == 0 && si >= 0;
+  const bool owner = pg == 0 && live && !qhalf;
+  const bool adam_here = owner && a.apply_adam;
   float pp = 0.f, pm = 0.f, pv = 0.f;
-  if (owner && a.apply_adam) {
+  if (adam_here) {
     pp = a.p[e];
     pm = a.m[e];
     pv = a.v[e];
@@ -65,39 +87,67 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   // only: the same pow in every wave costs more (11.4 us) than it hides.
   // (The code shape matters: an equivalent lambda form measured 10.1 us.)
   AdamCoef c{};
-  const bool adam_here = owner && a.apply_adam;
   bool coef_done = false;
-  if (si >= 0) {
-    const Seg& S = a.seg[si];
-    if (S.kind == 0) {
-      // fixed summation order (deterministic); UNR independent loads in flight
-      constexpr int UNR = 256 / RED_G;  // 256 slabs / RED_G groups: every load of a thread in flight at once
-      const float* base = a.slab[S.tower] + S.slab_off + (e - S.off);
-      const int n = S.n_slabs;
-      for (int p0 = pg; p0 < n; p0 += RED_G * UNR) {
-        float v[UNR];
+  int ch = 0, kx = 0;  // kinds 3, 4: W0 row / column of this element (kind 4: channel)
+  if (kind == 0 || kind == 3) {
+    constexpr int UNR = 256 / RED_G;  // 256 slabs / RED_G groups: every load of a thread in flight at once
+    int64_t so = live ? dv : 0;
+    if (kind == 3) {  // P[ch][kx] (or Q); group pg also takes replica pg of the fold sums
+      ch = wi / S.in;
+      kx = wi - ch * S.in;
+      if (!live) ch = kx = 0;
+      so = (int64_t)ch * 2 * S.kp + (kx >> 4) * 32 + (kx & 15) + (qhalf ? 16 : 0);
+      const float* fr = S.rep + (int64_t)pg * S.rep_stride;
+      xpart[0][pg][el] = fr[ch];
+      xpart[1][pg][el] = fr[H0 + ch];
+      xpart[2][pg][el] = fr[2 * H0 + ch];
+      xpart[3][pg][el] = fr[3 * H0 + kx];
+    }
+    // fixed summation order (deterministic); UNR independent loads in flight,
+    // buffer loads off the block-uniform slab base (32-bit lane offsets: half
+    // the address registers of 64-bit pointers)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.slab[S.tower] + S.slab_off), (short)0,
+                                                      0x7FFFFFFF, 0x00020000);
+    const uint32_t o0 = (uint32_t)so * 4u, ldb = (uint32_t)a.slab_ld * 4u;
+    auto ldp = [&](int p) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(o0 + (uint32_t)p * ldb), 0, 0)); };
+    const int n = S.n_slabs;
+    if (n <= RED_G * (UNR / 2)) {
+      // at most 128 slabs (k_top's and the folded k_bwd_mid's 128-row tiles
+      // at B = 16384): half the loads, none of them a clamped repeat
+      constexpr int U2 = UNR / 2;
+      float x[U2];
 #pragma unroll
-        for (int k = 0; k < UNR; ++k) {
-          const int p = min(p0 + k * RED_G, n - 1);
-          v[k] = base[(int64_t)p * a.slab_ld];
-        }
+      for (int k = 0; k < U2; ++k) x[k] = ldp(min(pg + k * RED_G, n - 1));
+      if (adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+      coef_done = true;
+#pragma unroll
+      for (int k = 0; k < U2; ++k) acc += (pg + k * RED_G < n) ? x[k] : 0.f;
+    } else {
+      for (int p0 = pg; p0 < n; p0 += RED_G * UNR) {
+        float x[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) x[k] = ldp(min(p0 + k * RED_G, n - 1));
         if (!coef_done) {
           if (adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
           coef_done = true;
         }
 #pragma unroll
-        for (int k = 0; k < UNR; ++k) acc += (p0 + k * RED_G < n) ? v[k] : 0.f;
-      }
-    } else if (S.kind == 1) {
-      if (pg == 0) acc = a.gacc[e];
-    } else {  // replicas: group pg sums replicas pg, pg + RED_G, ... (fixed order) and zeroes them
-      float* rp = S.rep + (e - S.off);
-#pragma unroll
-      for (int q = pg; q < NREP; q += RED_G) {
-        acc += rp[q * S.rep_stride];
-        rp[q * S.rep_stride] = 0.f;
+        for (int k = 0; k < UNR; ++k) acc += (p0 + k * RED_G < n) ? x[k] : 0.f;
       }
     }
+  } else if (kind == 1) {
+    if (pg == 0 && live) acc = a.gacc[e];
+  } else if (kind == 2) {  // replicas: group pg sums replica pg (fixed order), zeroes it
+    if (live) {
+      float* rp = S.rep + dv + (int64_t)pg * S.rep_stride;
+      acc = *rp;
+      if (!S.keep) *rp = 0.f;
+    }
+  } else {  // kind 4: b0 of the folded BN0 backward (replica pg of gg0 | sum Zh0)
+    ch = live ? (int)dv : 0;
+    const float* fr = S.rep + (int64_t)pg * S.rep_stride;
+    xpart[0][pg][el] = fr[ch];
+    xpart[2][pg][el] = fr[2 * H0 + ch];
   }
   if (!coef_done && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
   part[pg][el] = acc;
@@ -127,8 +177,31 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   float gsum = 0.f;
 #pragma unroll
   for (int k = 0; k < RED_G; ++k) gsum += part[k][el];
+  if (kind >= 3) {
+    // dW0 = k0 (P - mb s - mg Q) + db0 c,  db0 = -k0 mg sum Zh0  (k_bwd_mid_fold)
+    float gg = 0.f, zs = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < RED_G; ++k) {
+      gg += xpart[0][k][el];
+      zs += xpart[2][k][el];
+    }
+    const float k0 = S.k0[ch], mg = gg * a.inv_b;
+    const float db0 = -k0 * mg * zs;  // = sum over rows of dZ0 (BN0 cancels b0: ~0)
+    if (kind == 3) {
+      float q = 0.f, gb = 0.f, sx = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < RED_G; ++k) {
+        q += part[k][el + 16];
+        gb += xpart[1][k][el];
+        sx += xpart[3][k][el];
+      }
+      gsum = k0 * (gsum - (gb * a.inv_b) * sx - mg * q) + S.xsh[kx] * db0;
+    } else {
+      gsum = db0;
+    }
+  }
   a.grad[e] = gsum;
-  if (a.seg[si].kind == 1) a.gacc[e] = 0.f;
+  if (kind == 1) a.gacc[e] = 0.f;
   if (a.apply_adam) {
     adam_elem(pp, pm, pv, gsum, c);
     a.p[e] = pp;

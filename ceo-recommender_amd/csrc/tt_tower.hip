@@ -446,6 +446,13 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
     __syncthreads();
     if (threadIdx.x < 2 * H0) atomicAdd(&T.st0[rep_of_block() * 2 * H0 + threadIdx.x], red[threadIdx.x]);
   }
+  // the folded BN0 backward's replicas start every step at zero (k_bwd_mid
+  // accumulates them, k_reduce_adam only reads them)
+  if (a.fr_zero) {
+    const int nthr = (int)(gridDim.x * gridDim.y) * NTH;
+    for (int i = (int)((blockIdx.y * gridDim.x + blockIdx.x) * NTH + threadIdx.x); i < a.fr_zero_len; i += nthr)
+      a.fr_zero[i] = 0.f;
+  }
   TT_STAMP(0, 3);
 }
 
@@ -1203,6 +1210,305 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_bwd_mid_fold : k_bwd_mid with the BN0 backward and dW0 folded in, for
+// numeric-only towers with kp <= 64 (k_bwd_first is not launched).
+//
+// BN0's backward  dZ0 = k0 (dY0 - mb - Zh0 mg)  (k0 = inv0 gamma0,
+// mb = mean_B dY0, mg = mean_B dY0 Zh0) needs batch-wide means, but
+// dW0 = dZ0^T X is linear in them:
+//   dW0 = k0 (P - mb s^T - mg Q) + db0 c^T,   X' = X - c (c: the batch's
+//   first row, keeps the subtractions well conditioned),
+//   P = dY0^T X', Q = Zh0^T X', s = sum_rows X', db0 = -k0 mg sum_rows Zh0.
+// Each 128-row tile writes P and Q as slab partials (the same bytes per
+// batch row as k_bwd_first's dW0 partials of 64-row tiles) and s, sum Zh0,
+// dgamma0, dbeta0 into replicas; k_reduce_adam combines them with the batch
+// means (Seg kinds 3, 4).  dY0 never leaves the block.
+// 8 waves, wave w owns tile rows 16w..16w+15 (C layout) as in k_bwd_mid;
+// the rows-contracted products read row-major LDS operands
+// (strip_gemm_tn): dY0, Zh0 from the accumulator layout, X' from a
+// row-coalesced gather (16 lanes per 256-B row).
+// ---------------------------------------------------------------------------
+template <int R>
+struct FoldLds {
+  static constexpr int LDW = H0 + 4;       // W4 row-major [32][68]
+  static constexpr int LDT = R + 4;        // transposed images [col][row]
+  static constexpr int LDR = H0 + 4;       // row-major [row][68] images (dY0, Zh0, X')
+  static constexpr int W4s = 0;
+  static constexpr int dZT = W4s + H1 * LDW;
+  static constexpr int A0T = dZT + H1 * LDT;
+  static constexpr int dead = A0T + H0 * LDT;   // end of the region dead after dW4 / dA0
+  static constexpr int Zr = 0;                   // Zh0 row-major over the dead region
+  static_assert(R * LDR <= dead, "Zh0 image over W4s|dZT|A0T");
+  static constexpr int Yr = dead;                // dY0 row-major
+  static constexpr int Xr = Yr + R * LDR;        // X' row-major
+  static constexpr int db4 = Xr + R * LDR;       // [32]
+  static constexpr int c1 = db4 + H1;            // k1 mb mg mean1 inv1 [5][32]
+  static constexpr int c0 = c1 + 5 * H1;         // mean0 alpha0 beta0 inv0 [4][64]
+  static constexpr int red = c0 + 4 * H0;        // sum dY0 Zh0 | sum dY0 | sum Zh0 | sum X' [4][64]
+  static constexpr int rsc = red + 4 * H0;       // [4R] replica-sum scratch
+  static constexpr int rst = rsc + 4 * R;        // [2][32] sum dgamma1 | sum dbeta1
+  static constexpr int total = rst + 2 * H1;
+  static constexpr size_t bytes = sizeof(float) * (size_t)total;
+  static_assert(Yr % 4 == 0 && Xr % 4 == 0 && LDR % 4 == 0, "16-B rows");
+};
+
+template <int R, bool VEC>
+__global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
+  using L = FoldLds<R>;
+  static_assert(R == 128, "8 waves: one dW4 tile and one P|Q strip per wave");
+  constexpr int NTH = R * 4;
+  constexpr int LDW = L::LDW, LDT = L::LDT, LDR = L::LDR;
+  constexpr int XK = R * (FOLD_MAX_KP / 4) / NTH;  // X' float4 per thread (4)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int t = blockIdx.y;
+  const TowerDev& T = a.tw[t];
+  const int64_t step = step_current(a);
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
+  float* W4s = smem + L::W4s;
+  float* dZT = smem + L::dZT;
+  float* A0T = smem + L::A0T;
+  float* db4 = smem + L::db4;
+  float* c1 = smem + L::c1;
+  float* c0 = smem + L::c0;
+  float* red = smem + L::red;
+  TT_STAMP(3, 0);
+
+  // ---- phase 0: issue every load -- dY1, Z4, Z0 of this wave's rows (C
+  // layout), W4, BN inputs, then (after the step load they depend on) the
+  // dataset rows of this thread's X' gather rows and of the shift row
+  f32x4 dy1[2], zz4[2], zz0[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = r0 + 16 * w + 4 * g + i;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      dy1[q][i] = T.dY1[row * H1 + 16 * q + r];
+      zz4[q][i] = T.Z4[row * H1 + 16 * q + r];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) zz0[j][i] = T.Z0[row * H0 + 16 * j + r];
+  }
+  static_assert(H1 * H0 / 4 == NTH, "W4: one float4 per thread");
+  const int we = (int)threadIdx.x;
+  const float4 w4v = *reinterpret_cast<const float4*>(T.W4 + (we >> 4) * H0 + 4 * (we & 15));
+  const int c1i = min((int)threadIdx.x, H1 - 1), c0i = min(max((int)threadIdx.x - H1, 0), H0 - 1);
+  const float f1inv = T.fin1[H1 + c1i], f1mean = T.fin1[c1i], g1v = T.g1[c1i];
+  const float f0inv = T.fin0[H0 + c0i], f0mean = T.fin0[c0i], g0v = T.g0[c0i], be0v = T.be0[c0i];
+  const float invB = 1.f / (float)a.B;
+  // X' gather: thread takes float4 column group xc of rows xr0 + 32k
+  const int xc = (int)threadIdx.x & 15, xr0 = (int)threadIdx.x >> 4;
+  const int64_t base = batch_row0(a, step);
+  int64_t xrow[XK];
+#pragma unroll
+  for (int k = 0; k < XK; ++k) xrow[k] = data_row_nb(a, base, min(r0 + xr0 + 32 * k, a.B - 1));
+  const int64_t crow = data_row_nb(a, base, 0);
+  rep_sum<NTH, 2 * H1>(T.gg1, BNG, smem + L::rsc, smem + L::rst);  // gg1|gbe1 are adjacent in a replica
+  {
+    const float* rst = smem + L::rst;
+    if (threadIdx.x < H1) {
+      const int c = threadIdx.x;
+      c1[c] = f1inv * g1v;
+      c1[H1 + c] = rst[H1 + c] * invB;
+      c1[2 * H1 + c] = rst[c] * invB;
+      c1[3 * H1 + c] = f1mean;
+      c1[4 * H1 + c] = f1inv;
+    } else if (threadIdx.x < H1 + H0) {
+      const int c = threadIdx.x - H1;
+      c0[c] = f0mean;
+      c0[H0 + c] = f0inv * g0v;
+      c0[2 * H0 + c] = be0v;
+      c0[3 * H0 + c] = f0inv;
+    }
+  }
+  if (threadIdx.x < H1) db4[threadIdx.x] = 0.f;
+  if (threadIdx.x < 4 * H0) red[threadIdx.x] = 0.f;
+  *reinterpret_cast<float4*>(W4s + (we >> 4) * LDW + 4 * (we & 15)) = w4v;
+  __syncthreads();
+  TT_STAMP(3, 1);
+
+  // ---- phase 1: X' gather issued (used in phase 3: its latency hides
+  // behind this phase's arithmetic), dZ4, A0 / Zh0 recompute
+  // (VEC a template argument: a load under a run-time branch would make hipcc
+  // wait for it at the join, exposing the gather here)
+  const int n4 = VEC ? (T.n_num >> 2) : 0;
+  const int xcl = min(xc, max(n4 - 1, 0));
+  float4 xv[XK], cv;
+  if constexpr (VEC) {
+#pragma unroll
+    for (int k = 0; k < XK; ++k) xv[k] = *reinterpret_cast<const float4*>(T.num + xrow[k] * T.num_ld + 4 * xcl);
+    cv = *reinterpret_cast<const float4*>(T.num + crow * T.num_ld + 4 * xcl);
+  } else {
+    const int nn = T.n_num;
+    auto ld1 = [&](int64_t drow, int col) { return T.num[drow * T.num_ld + min(col, nn - 1)]; };
+#pragma unroll
+    for (int k = 0; k < XK; ++k)
+      xv[k] = make_float4(ld1(xrow[k], 4 * xc), ld1(xrow[k], 4 * xc + 1), ld1(xrow[k], 4 * xc + 2),
+                          ld1(xrow[k], 4 * xc + 3));
+    cv = make_float4(ld1(crow, 4 * xc), ld1(crow, 4 * xc + 1), ld1(crow, 4 * xc + 2), ld1(crow, 4 * xc + 3));
+  }
+
+  f32x4 dz[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int col = 16 * q + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = r0 + 16 * w + 4 * g + i;
+      const float zh = (zz4[q][i] - c1[3 * H1 + col]) * c1[4 * H1 + col];
+      const float v = c1[col] * (dy1[q][i] - c1[H1 + col] - zh * c1[2 * H1 + col]);
+      dz[q][i] = row < a.B ? v : 0.f;
+    }
+    store_tile_T(dZT, LDT, 16 * q, 16 * w, dz[q]);
+    const float cb = col_reduce(dz[q][0] + dz[q][1] + dz[q][2] + dz[q][3]);
+    if (g == 0) atomicAdd(db4 + col, cb);
+  }
+  const bool drop = a.drop_thr > 0;
+  const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
+  f32x4 a0[4], zh0[4];
+  uint32_t rk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) rk[i] = dropout_row_key(key, r0 + 16 * w + 4 * g + i);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = 16 * j + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = r0 + 16 * w + 4 * g + i;
+      const float z = zz0[j][i];
+      const bool ok = row < a.B;
+      const float av = bn_relu_drop(z, c0[col], c0[H0 + col], c0[2 * H0 + col], drop, rk[i], col, a.drop_thr,
+                                    a.drop_scale);
+      a0[j][i] = ok ? av : 0.f;
+      zh0[j][i] = ok ? (z - c0[col]) * c0[3 * H0 + col] : 0.f;
+    }
+    store_tile_T(A0T, LDT, 16 * j, 16 * w, a0[j]);
+  }
+  __syncthreads();
+  TT_STAMP(3, 2);
+
+  // ---- phase 2: dW4 = dZ4^T A0 (wave w: h1-tile w & 1, h0-tile w >> 1),
+  // dA0 = dZ4 W4 on the wave's rows -> dY0, BN0-backward column partials
+  float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
+  {
+    const int p = w & 1, q = w >> 1;
+    f32x4 acc[1] = {zero4()};
+    strip_gemm_nt<1>(dZT + 16 * p * LDT, LDT, A0T + 16 * q * LDT, LDT, R, acc);
+    store_tile_rm_wt(slab, (int)T.so_W4 + 16 * p * H0 + 16 * q, H0, acc[0]);
+  }
+  f32x4 dA[4] = {zero4(), zero4(), zero4(), zero4()};
+  strip_gemm_tn<4>(dZT + 16 * w, LDT, W4s, LDW, H1, dA);
+  const float scl = drop ? a.drop_scale : 1.f;
+  float sg[4], sb[4], sz[4];
+  f32x4 dyt[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sg[j] = 0.f;
+    sb[j] = 0.f;
+    sz[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float dy = a0[j][i] > 0.f ? dA[j][i] * scl : 0.f;  // 0 on rows >= B (a0 = 0)
+      dyt[j][i] = dy;
+      sg[j] += dy * zh0[j][i];
+      sb[j] += dy;
+      sz[j] += zh0[j][i];
+    }
+  }
+  cols_to_lds<4>(sg, red);
+  cols_to_lds<4>(sb, red + H0);
+  cols_to_lds<4>(sz, red + 2 * H0);
+  __syncthreads();  // every wave is past dW4 (A0T) and dA0 (W4s, dZT)
+  TT_STAMP(3, 3);
+
+  // ---- phase 3: row-major images dY0, Zh0 (over the dead region), X'
+  {
+    float* Yr = smem + L::Yr;
+    float* Zr = smem + L::Zr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rw = 16 * w + 4 * g + i;
+        Yr[rw * LDR + 16 * j + r] = dyt[j][i];
+        Zr[rw * LDR + 16 * j + r] = zh0[j][i];
+      }
+    // X' = X - c on valid rows and columns, 0 elsewhere; column partial sums
+    const bool cok = xc < ((T.n_num + 3) >> 2);
+    float4 sxv = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const int rw = xr0 + 32 * k;
+      const bool ok = cok && r0 + rw < a.B;
+      float4 d = make_float4(xv[k].x - cv.x, xv[k].y - cv.y, xv[k].z - cv.z, xv[k].w - cv.w);
+      if constexpr (!VEC) {  // ragged last group of an unaligned width
+        const int c = 4 * xc;
+        d.x = c + 0 < T.n_num ? d.x : 0.f;
+        d.y = c + 1 < T.n_num ? d.y : 0.f;
+        d.z = c + 2 < T.n_num ? d.z : 0.f;
+        d.w = c + 3 < T.n_num ? d.w : 0.f;
+      }
+      d = ok ? d : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(smem + L::Xr + rw * LDR + 4 * xc) = d;
+      sxv.x += d.x;
+      sxv.y += d.y;
+      sxv.z += d.z;
+      sxv.w += d.w;
+    }
+    // lanes xc, xc + 16, xc + 32, xc + 48 share a column group
+    const float s0 = col_reduce(sxv.x), s1 = col_reduce(sxv.y), s2 = col_reduce(sxv.z), s3 = col_reduce(sxv.w);
+    if (g == 0) {
+      float* rs = red + 3 * H0 + 4 * xc;
+      atomicAdd(rs + 0, s0);
+      atomicAdd(rs + 1, s1);
+      atomicAdd(rs + 2, s2);
+      atomicAdd(rs + 3, s3);
+    }
+    if (blockIdx.x == 0) {  // inv0 * gamma0 and the shift row for k_reduce_adam
+      if (threadIdx.x < H0) T.k0s[threadIdx.x] = c0[H0 + threadIdx.x];
+      if (threadIdx.x < 16) {
+        float4 c = cv;
+        if (!cok) c = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(T.xsh + 4 * xc) = c;
+      }
+    }
+  }
+  __syncthreads();
+  TT_STAMP(3, 4);
+
+  // ---- phase 4: P | Q = [dY0 | Zh0]^T X' over the tile's rows: wave w owns
+  // channels 16 (w & 3) .. +15 of P (w < 4) or Q, every column tile.  Slab
+  // layout [64][kp/16][P 16 | Q 16]: k_reduce_adam's lanes for 16 columns of
+  // P and the same 16 of Q read one contiguous 128 B
+  {
+    const float* As = smem + (w < 4 ? L::Yr : L::Zr) + 16 * (w & 3);
+    const int kp = T.kp, KT = kp / 16;
+    const int so = (int)T.so_W0 + 16 * (w & 3) * 2 * kp + (w < 4 ? 0 : 16);
+    if (KT == 4) {
+      f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+      strip_gemm_tn<4>(As, LDR, smem + L::Xr, LDR, R, acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) store_tile_rm_wt(slab, so + 32 * q, 2 * kp, acc[q]);
+    } else {
+      for (int kt = 0; kt < KT; ++kt) {
+        f32x4 acc[1] = {zero4()};
+        strip_gemm_tn<1>(As, LDR, smem + L::Xr + 16 * kt, LDR, R, acc);
+        store_tile_rm_wt(slab, so + 32 * kt, 2 * kp, acc[0]);
+      }
+    }
+  }
+  if (threadIdx.x < H0) {
+    float* fr = T.fr + rep_of_block() * FRW;
+    atomicAdd(fr + threadIdx.x, red[threadIdx.x]);                    // gamma0 grad
+    atomicAdd(fr + H0 + threadIdx.x, red[H0 + threadIdx.x]);          // beta0 grad
+    atomicAdd(fr + 2 * H0 + threadIdx.x, red[2 * H0 + threadIdx.x]);  // sum Zh0
+    atomicAdd(fr + 3 * H0 + threadIdx.x, red[3 * H0 + threadIdx.x]);  // sum X'
+  }
+  if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = db4[threadIdx.x];
+  TT_STAMP(3, 5);
+}
+
+// ---------------------------------------------------------------------------
 // k_bwd_first : BN0 backward -> dZ0 ; dW0 = dZ0^T X ; db0 ; dX -> embedding grads
 // ---------------------------------------------------------------------------
 template <int R>
@@ -1432,6 +1738,8 @@ template __global__ void k_top<8, 64, true>(StepArgs);
 template __global__ void k_top<4, 128, true>(StepArgs);
 template __global__ void k_top<8, 128, true>(StepArgs);
 template __global__ void k_bwd_mid<64>(StepArgs);
+template __global__ void k_bwd_mid_fold<128, true>(StepArgs);
+template __global__ void k_bwd_mid_fold<128, false>(StepArgs);
 template __global__ void k_bwd_first<64>(StepArgs);
 
 }  // namespace tt

@@ -5,6 +5,6 @@ R=$1; shift
 for i in $(seq 1 $R); do
   for L in "$@"; do
     CEO_TT_LIB=ceo-recommender_amd/lib/$L timeout -k 10 200 python bench.py --no-cpu-baseline --no-contrastive --steps 400 > gpurun_out/bm/$L.$i.json 2> gpurun_out/bm/$L.$i.err || { echo "$L failed"; tail -5 gpurun_out/bm/$L.$i.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/bm/$L.$i.json'));k=d['kernel_us'];print('$L', d['ms_per_step'], round(d['value']/1e6,1), 'reduce', k['k_reduce_adam'], 'top', k['k_top'])"
+    python -c "import json;d=json.load(open('gpurun_out/bm/$L.$i.json'));k=d['kernel_us'];print('$L', d['ms_per_step'], round(d['value']/1e6,1), {a[2:]: round(b,2) for a,b in k.items()})"
   done
 done

@@ -48,30 +48,39 @@ PEAK_FP32_TFLOPS = 157.3     # dense fp32 (vector == MFMA f32) spec
 # 2.4 GHz) over the 6 plane products of the bf16x3 split = the fp32-equivalent
 # ceiling of the contrastive GEMM core
 PEAK_BF16X3_TFLOPS = round(2516.6 / 6, 1)
+# event slots of tt_train_step_ev (slot 4 stays unrecorded when the BN0
+# backward is folded into k_bwd_mid: tt_step_plan)
 KERNELS = ("k_l0_fwd", "k_l4_fwd", "k_top", "k_bwd_mid", "k_bwd_first", "k_reduce_adam")
 
 
-def kernel_work(nf, nc, D, B, n_params, n_tiles):
+def kernel_work(nf, nc, D, B, n_params, plan):
     """Algorithmic FLOPs and HBM bytes per launch of each step kernel
     (both towers; FLOPs count 2 per multiply-add; bytes = compulsory
-    activation / input / partial traffic, fp32)."""
+    activation / input / partial-slab traffic, fp32).  plan: tt_step_plan."""
     f = 4
+    kp = lambda n: -(-n // 16) * 16  # noqa: E731
+    tiles = lambda rows: -(-B // rows)  # noqa: E731
+    t64, ttop, tmid = tiles(64), tiles(plan["top_rows"]), tiles(plan["mid_rows"])
+    fold = plan["folded_bn0_backward"]
     fl = {
         "k_l0_fwd": 2 * B * 64 * (nf + nc),
         "k_l4_fwd": 2 * 2 * B * 32 * 64,
         "k_top": 2 * (3 * B * D * 32) * 2,          # U,V fwd + dW8 + dA1, both towers
-        "k_bwd_mid": 2 * 2 * (2 * B * 32 * 64),     # dW4 + dA0
-        "k_bwd_first": 2 * B * 64 * (nf + nc),      # dW0
+        "k_bwd_mid": 2 * 2 * (2 * B * 32 * 64)      # dW4 + dA0
+                     + (2 * 2 * B * 64 * (nf + nc) if fold else 0),  # P, Q (folded dW0)
+        "k_bwd_first": 0 if fold else 2 * B * 64 * (nf + nc),        # dW0
         "k_reduce_adam": 0,
     }
-    slab_w = lambda n: n_tiles * n * f  # noqa: E731
+    w0_slab = (2 * 64 * (kp(nf) + kp(nc)) * 2) if fold else (64 * (nf + nc) + 128)
     by = {
         "k_l0_fwd": B * (nf + nc) * f + 2 * B * 64 * f,
         "k_l4_fwd": 2 * B * 64 * f + 2 * B * 32 * f,
-        "k_top": 2 * B * 32 * f + 2 * B * f + 2 * B * 32 * f + slab_w(2 * (D * 32 + D)),
-        "k_bwd_mid": 2 * B * 32 * f * 2 + 2 * B * 64 * f * 2 + slab_w(2 * (32 * 64 + 32)),
-        "k_bwd_first": 2 * B * 64 * f * 2 + B * (nf + nc) * f + slab_w(64 * (nf + nc) + 128),
-        "k_reduce_adam": slab_w(n_params) + 7 * n_params * f,
+        "k_top": 2 * B * 32 * f + 2 * B * f + 2 * B * 32 * f + ttop * 2 * (D * 32 + D) * f,
+        "k_bwd_mid": (2 * B * 32 * f * 2 + 2 * B * 64 * f + tmid * 2 * (32 * 64 + 32) * f
+                      + ((B * (nf + nc) * f + tmid * w0_slab * f) if fold else 2 * B * 64 * f)),
+        "k_bwd_first": 0 if fold else 2 * B * 64 * f * 2 + B * (nf + nc) * f + t64 * w0_slab * f,
+        "k_reduce_adam": (ttop * 2 * (D * 32 + D) + tmid * 2 * (32 * 64 + 32)
+                          + (tmid if fold else t64) * w0_slab) * f + 7 * n_params * f,
     }
     return fl, by
 
@@ -499,10 +508,16 @@ def main():
             if pg is not None:
                 tr.allreduce_and_adam()
         torch.cuda.synchronize()
+        plan = N.step_plan(tr.desc, B)
         per = {}
         for i, name in enumerate(KERNELS):
+            if name == "k_bwd_first" and plan["folded_bn0_backward"]:
+                continue  # not launched: its work runs inside k_bwd_mid (folded BN0 backward)
             per[name] = sum(evs[k][2 * i].elapsed_time(evs[k][2 * i + 1]) for k in range(args.steps)) / args.steps * 1e3
-        fl, by = kernel_work(nf, nc, D, B, a.params.numel(), -(-B // 64))
+        fl, by = kernel_work(nf, nc, D, B, a.params.numel(), plan)
+        if plan["folded_bn0_backward"]:  # report the kernel that ran under its own name
+            for d_ in (per, fl, by):
+                d_["k_bwd_mid_fold"] = d_.pop("k_bwd_mid")
         dom = max(per, key=per.get)
         t_s = per[dom] * 1e-6
         tf = fl[dom] / t_s / 1e12
@@ -518,6 +533,7 @@ def main():
         roof["traffic"] = load_pmc_traffic(dom)
         result["roofline"] = roof
         result["kernel_us"] = {k: round(v, 3) for k, v in per.items()}
+        result["step_plan"] = plan
         result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)
         if rank == 0:
             result["cosine_roofline"] = cosine_roofline(dev, D=D)

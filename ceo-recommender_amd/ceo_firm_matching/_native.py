@@ -32,7 +32,7 @@ EXPORTED = ("tt_abi_version", "tt_param_count", "tt_param_offsets", "tt_buffer_c
             "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_train_step", "tt_train_step_ev",
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
             "tt_nce_workspace_bytes", "tt_nce_norms", "tt_nce_forward", "tt_nce_loss", "tt_nce_backward",
-            "tt_rank_workspace_bytes", "tt_retrieval_ranks")
+            "tt_rank_workspace_bytes", "tt_retrieval_ranks", "tt_step_plan")
 
 
 class NativeLibraryError(RuntimeError):
@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
         "tt_rank_workspace_bytes": (I64, [I64]),
         "tt_retrieval_ranks": (I32, [P, P, I64, I64, I32, I64, P, I64, P, P]),
         "tt_ar_region_bytes": (I64, [I64]),
+        "tt_step_plan": (I32, [ctypes.POINTER(TTModelDesc), I64, P, I32]),
         "tt_ar_alloc": (I32, [I64, ctypes.POINTER(P), P]),
         "tt_ar_open": (I32, [P, ctypes.POINTER(P)]),
         "tt_ar_close": (I32, [P]),
@@ -167,6 +168,13 @@ def make_desc(n_num: Sequence[int], cat_counts: Sequence[Sequence[int]],
     d.bn_eps = float(bn_eps)
     d.bn_momentum = float(bn_momentum)
     return d
+
+
+def step_plan(desc: TTModelDesc, batch: int) -> dict:
+    """How one fused training step runs at this batch size (tt_step_plan)."""
+    info = (ctypes.c_int32 * 4)()
+    check(lib().tt_step_plan(ctypes.byref(desc), int(batch), info, 4), "tt_step_plan")
+    return {"folded_bn0_backward": bool(info[0]), "top_rows": info[1], "mid_rows": info[2], "kernels": info[3]}
 
 
 def param_count(desc: TTModelDesc) -> int:

@@ -466,15 +466,10 @@ static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev =
   else
     launch(k_bwd_mid_fold<FOLD_ROWS, false>, grid, blk, P.lds_mid, s, ev, a);
 }
-// folded BN0 backward: nothing to launch (the events, when given, bracket nothing)
+// folded BN0 backward: nothing to launch (its event pair stays unrecorded:
+// tt_step_plan tells the caller which kernels a step runs)
 static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
-  if (a.fr_zero) {
-    if (ev.e0 && ev.e1) {
-      (void)hipEventRecord(ev.e0, s);
-      (void)hipEventRecord(ev.e1, s);
-    }
-    return;
-  }
+  if (a.fr_zero) return;
   launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
 static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}) {
@@ -521,6 +516,19 @@ int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out) {
   for (int t = 0; t < 2; ++t)
     for (int s = 0; s < TT_SLOTS_PER_TOWER; ++s) out[2 * TT_MAX_CAT + t * TT_SLOTS_PER_TOWER + s] = L.slot[t][s];
   out[2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER] = L.ls;
+  return TT_OK;
+}
+
+int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32_t n_info) {
+  if (!desc_ok(d) || batch < 1 || !info || n_info < 4) return TT_ERR_ARG;
+  const Layout L = make_layout(d);
+  Plan P;
+  const int rc = make_plan(d, L, batch, &P);
+  if (rc) return rc;
+  info[0] = L.fold ? 1 : 0;
+  info[1] = P.top_rows;
+  info[2] = L.fold ? FOLD_ROWS : ROWS;
+  info[3] = L.fold ? 5 : 6;
   return TT_OK;
 }
 

@@ -576,8 +576,11 @@ constexpr int MAX_SEG = 48;
 #ifndef TT_RED_MINW
 #define TT_RED_MINW 7  // waves per SIMD: <= 73 VGPRs (no spills with 16 loads in flight); 9.4 us vs 10.8 at 8
 #endif
-constexpr int RED_E = 32;  // elements per k_reduce_adam block
-constexpr int RED_G = 16;  // slab groups per element (512 threads, 16 slab loads each)
+#ifndef TT_RED_E
+#define TT_RED_E 64  // 64 x 8: 8.1 us vs 9.4 at 32 x 16 (cfg3, folded: every range <= 128 slabs)
+#endif
+constexpr int RED_E = TT_RED_E;    // elements per k_reduce_adam block
+constexpr int RED_G = 512 / RED_E; // slab groups per element (512 threads, 16 slab loads in flight each)
 
 struct Seg {
   int64_t off, len;      // range in the parameter arena

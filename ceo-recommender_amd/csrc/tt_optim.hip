@@ -49,8 +49,8 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // elements -- so the owner finds both sums in this block's LDS and every lane
 // reads 64 B of one 128-B P|Q row segment.
 __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedArgs a) {
-  static_assert(RED_G == NREP, "kinds 3, 4: group pg takes replica pg");
-  static_assert(RED_E == 32, "kind 3 pairs lanes el and el + 16");
+  static_assert(NREP % RED_G == 0, "kinds 2-4: group pg takes replicas pg, pg + RED_G, ...");
+  static_assert(RED_E % 32 == 0, "kind 3 pairs lanes el and el + 16 of a 32-lane group");
   __shared__ float part[RED_G][RED_E];
   __shared__ float xpart[4][RED_G][RED_E];  // kinds 3, 4: gg0, gbe0, sum Zh0, sum X' replicas
   TT_STAMP(5, 0);
@@ -90,18 +90,26 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   bool coef_done = false;
   int ch = 0, kx = 0;  // kinds 3, 4: W0 row / column of this element (kind 4: channel)
   if (kind == 0 || kind == 3) {
-    constexpr int UNR = 256 / RED_G;  // 256 slabs / RED_G groups: every load of a thread in flight at once
+    constexpr int UNR = 16;  // slab loads in flight per lane
     int64_t so = live ? dv : 0;
     if (kind == 3) {  // P[ch][kx] (or Q); group pg also takes replica pg of the fold sums
       ch = wi / S.in;
       kx = wi - ch * S.in;
       if (!live) ch = kx = 0;
       so = (int64_t)ch * 2 * S.kp + (kx >> 4) * 32 + (kx & 15) + (qhalf ? 16 : 0);
-      const float* fr = S.rep + (int64_t)pg * S.rep_stride;
-      xpart[0][pg][el] = fr[ch];
-      xpart[1][pg][el] = fr[H0 + ch];
-      xpart[2][pg][el] = fr[2 * H0 + ch];
-      xpart[3][pg][el] = fr[3 * H0 + kx];
+      float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
+#pragma unroll
+      for (int q = pg; q < NREP; q += RED_G) {
+        const float* fr = S.rep + (int64_t)q * S.rep_stride;
+        r0 += fr[ch];
+        r1 += fr[H0 + ch];
+        r2 += fr[2 * H0 + ch];
+        r3 += fr[3 * H0 + kx];
+      }
+      xpart[0][pg][el] = r0;
+      xpart[1][pg][el] = r1;
+      xpart[2][pg][el] = r2;
+      xpart[3][pg][el] = r3;
     }
     // fixed summation order (deterministic); UNR independent loads in flight,
     // buffer loads off the block-uniform slab base (32-bit lane offsets: half
@@ -112,8 +120,8 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
     auto ldp = [&](int p) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(o0 + (uint32_t)p * ldb), 0, 0)); };
     const int n = S.n_slabs;
     if (n <= RED_G * (UNR / 2)) {
-      // at most 128 slabs (k_top's and the folded k_bwd_mid's 128-row tiles
-      // at B = 16384): half the loads, none of them a clamped repeat
+      // few slabs for this block shape (e.g. 128-row tiles at B = 16384 with
+      // 16 groups): half the loads, none of them a clamped repeat
       constexpr int U2 = UNR / 2;
       float x[U2];
 #pragma unroll
@@ -137,17 +145,26 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
     }
   } else if (kind == 1) {
     if (pg == 0 && live) acc = a.gacc[e];
-  } else if (kind == 2) {  // replicas: group pg sums replica pg (fixed order), zeroes it
+  } else if (kind == 2) {  // replicas: group pg sums replicas pg, pg + RED_G, ... (fixed order), zeroes them
     if (live) {
-      float* rp = S.rep + dv + (int64_t)pg * S.rep_stride;
-      acc = *rp;
-      if (!S.keep) *rp = 0.f;
+#pragma unroll
+      for (int q = pg; q < NREP; q += RED_G) {
+        float* rp = S.rep + dv + (int64_t)q * S.rep_stride;
+        acc += *rp;
+        if (!S.keep) *rp = 0.f;
+      }
     }
   } else {  // kind 4: b0 of the folded BN0 backward (replica pg of gg0 | sum Zh0)
     ch = live ? (int)dv : 0;
-    const float* fr = S.rep + (int64_t)pg * S.rep_stride;
-    xpart[0][pg][el] = fr[ch];
-    xpart[2][pg][el] = fr[2 * H0 + ch];
+    float r0 = 0.f, r2 = 0.f;
+#pragma unroll
+    for (int q = pg; q < NREP; q += RED_G) {
+      const float* fr = S.rep + (int64_t)q * S.rep_stride;
+      r0 += fr[ch];
+      r2 += fr[2 * H0 + ch];
+    }
+    xpart[0][pg][el] = r0;
+    xpart[2][pg][el] = r2;
   }
   if (!coef_done && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
   part[pg][el] = acc;

@@ -1223,25 +1223,29 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
 // batch row as k_bwd_first's dW0 partials of 64-row tiles) and s, sum Zh0,
 // dgamma0, dbeta0 into replicas; k_reduce_adam combines them with the batch
 // means (Seg kinds 3, 4).  dY0 never leaves the block.
-// 8 waves, wave w owns tile rows 16w..16w+15 (C layout) as in k_bwd_mid;
-// the rows-contracted products read row-major LDS operands
-// (strip_gemm_tn): dY0, Zh0 from the accumulator layout, X' from a
-// row-coalesced gather (16 lanes per 256-B row).
+// 8 waves, wave w owns tile rows 16w..16w+15 (C layout) as in k_bwd_mid.
+// P and Q run on the bf16x3 MFMA core (fp32-accurate, tt_common.h) from
+// channel-major bf16 plane images: dY0 / Zh0 written from the accumulator
+// layout, X' from a row-coalesced gather (16 lanes per 256-B row, each lane a
+// 4-row x 4-column block, so every image write is one 8-B chunk per plane).
 // ---------------------------------------------------------------------------
 template <int R>
 struct FoldLds {
   static constexpr int LDW = H0 + 4;       // W4 row-major [32][68]
   static constexpr int LDT = R + 4;        // transposed images [col][row]
-  static constexpr int LDR = H0 + 4;       // row-major [row][68] images (dY0, Zh0, X')
   static constexpr int W4s = 0;
   static constexpr int dZT = W4s + H1 * LDW;
   static constexpr int A0T = dZT + H1 * LDT;
   static constexpr int dead = A0T + H0 * LDT;   // end of the region dead after dW4 / dA0
-  static constexpr int Zr = 0;                   // Zh0 row-major over the dead region
-  static_assert(R * LDR <= dead, "Zh0 image over W4s|dZT|A0T");
-  static constexpr int Yr = dead;                // dY0 row-major
-  static constexpr int Xr = Yr + R * LDR;        // X' row-major
-  static constexpr int db4 = Xr + R * LDR;       // [32]
+  // phase 3-4 (over the dead region and beyond): the bf16x3 images of dY0,
+  // Zh0 and X', channel / column major ([64][R] bf16 per plane, rows along
+  // the contraction), 16-B chunks XOR-swizzled by the row's low 4 bits
+  static constexpr int PL = H0 * R;              // one plane, bf16 units
+  static constexpr int img = 3 * PL;             // one image (3 planes)
+  static constexpr int IY = 0, IZ = img, IX = 2 * img;
+  static constexpr int imgs_f = 3 * img / 2;     // floats
+  static_assert(imgs_f >= dead, "images cover the dead region");
+  static constexpr int db4 = imgs_f;             // [32]
   static constexpr int c1 = db4 + H1;            // k1 mb mg mean1 inv1 [5][32]
   static constexpr int c0 = c1 + 5 * H1;         // mean0 alpha0 beta0 inv0 [4][64]
   static constexpr int red = c0 + 4 * H0;        // sum dY0 Zh0 | sum dY0 | sum Zh0 | sum X' [4][64]
@@ -1249,15 +1253,18 @@ struct FoldLds {
   static constexpr int rst = rsc + 4 * R;        // [2][32] sum dgamma1 | sum dbeta1
   static constexpr int total = rst + 2 * H1;
   static constexpr size_t bytes = sizeof(float) * (size_t)total;
-  static_assert(Yr % 4 == 0 && Xr % 4 == 0 && LDR % 4 == 0, "16-B rows");
+  static_assert(R == 128, "16 chunks of 8 rows per image row: the swizzle covers a whole row");
 };
+
+// bf16 offset of (row c, contraction index k) in a FoldLds image plane
+__device__ __forceinline__ int fold_at(int c, int k) { return c * 128 + ((((k >> 3) ^ c) & 15) << 3) + (k & 7); }
 
 template <int R, bool VEC>
 __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   using L = FoldLds<R>;
   static_assert(R == 128, "8 waves: one dW4 tile and one P|Q strip per wave");
   constexpr int NTH = R * 4;
-  constexpr int LDW = L::LDW, LDT = L::LDT, LDR = L::LDR;
+  constexpr int LDW = L::LDW, LDT = L::LDT;
   constexpr int XK = R * (FOLD_MAX_KP / 4) / NTH;  // X' float4 per thread (4)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
@@ -1296,12 +1303,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   const float f1inv = T.fin1[H1 + c1i], f1mean = T.fin1[c1i], g1v = T.g1[c1i];
   const float f0inv = T.fin0[H0 + c0i], f0mean = T.fin0[c0i], g0v = T.g0[c0i], be0v = T.be0[c0i];
   const float invB = 1.f / (float)a.B;
-  // X' gather: thread takes float4 column group xc of rows xr0 + 32k
-  const int xc = (int)threadIdx.x & 15, xr0 = (int)threadIdx.x >> 4;
+  // X' gather: thread takes float4 column group xc of rows xr0 .. xr0 + 3
+  static_assert(XK == 4, "4 x 4 block per thread");
+  const int xc = (int)threadIdx.x & 15, xr0 = 4 * ((int)threadIdx.x >> 4);
   const int64_t base = batch_row0(a, step);
   int64_t xrow[XK];
 #pragma unroll
-  for (int k = 0; k < XK; ++k) xrow[k] = data_row_nb(a, base, min(r0 + xr0 + 32 * k, a.B - 1));
+  for (int k = 0; k < XK; ++k) xrow[k] = data_row_nb(a, base, min(r0 + xr0 + k, a.B - 1));
   const int64_t crow = data_row_nb(a, base, 0);
   rep_sum<NTH, 2 * H1>(T.gg1, BNG, smem + L::rsc, smem + L::rst);  // gg1|gbe1 are adjacent in a replica
   {
@@ -1421,48 +1429,43 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   __syncthreads();  // every wave is past dW4 (A0T) and dA0 (W4s, dZT)
   TT_STAMP(3, 3);
 
-  // ---- phase 3: row-major images dY0, Zh0 (over the dead region), X'
+  // ---- phase 3: bf16x3 images of dY0, Zh0 (from the accumulator layout:
+  // channel 16j + r, rows 16w + 4g .. +3) and X' (columns 4xc .. +3 of rows
+  // xr0 .. +3); the images overwrite the dead f32 region
   {
-    float* Yr = smem + L::Yr;
-    float* Zr = smem + L::Zr;
+    uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rw = 16 * w + 4 * g + i;
-        Yr[rw * LDR + 16 * j + r] = dyt[j][i];
-        Zr[rw * LDR + 16 * j + r] = zh0[j][i];
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int c = 16 * j + r, o = fold_at(c, 16 * w + 4 * g);
+      put_planes4(hs + L::IY + o, L::PL, make_float4(dyt[j][0], dyt[j][1], dyt[j][2], dyt[j][3]));
+      put_planes4(hs + L::IZ + o, L::PL, make_float4(zh0[j][0], zh0[j][1], zh0[j][2], zh0[j][3]));
+    }
     // X' = X - c on valid rows and columns, 0 elsewhere; column partial sums
     const bool cok = xc < ((T.n_num + 3) >> 2);
-    float4 sxv = make_float4(0.f, 0.f, 0.f, 0.f);
+    float d[XK][4];
 #pragma unroll
     for (int k = 0; k < XK; ++k) {
-      const int rw = xr0 + 32 * k;
-      const bool ok = cok && r0 + rw < a.B;
-      float4 d = make_float4(xv[k].x - cv.x, xv[k].y - cv.y, xv[k].z - cv.z, xv[k].w - cv.w);
-      if constexpr (!VEC) {  // ragged last group of an unaligned width
-        const int c = 4 * xc;
-        d.x = c + 0 < T.n_num ? d.x : 0.f;
-        d.y = c + 1 < T.n_num ? d.y : 0.f;
-        d.z = c + 2 < T.n_num ? d.z : 0.f;
-        d.w = c + 3 < T.n_num ? d.w : 0.f;
+      const bool ok = cok && r0 + xr0 + k < a.B;
+      const float x4[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w}, c4[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ci = VEC || 4 * xc + i < T.n_num;  // ragged last group of an unaligned width
+        d[k][i] = (ok && ci) ? x4[i] - c4[i] : 0.f;
       }
-      d = ok ? d : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(smem + L::Xr + rw * LDR + 4 * xc) = d;
-      sxv.x += d.x;
-      sxv.y += d.y;
-      sxv.z += d.z;
-      sxv.w += d.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 4 * xc + i;
+      put_planes4(hs + L::IX + fold_at(c, xr0), L::PL, make_float4(d[0][i], d[1][i], d[2][i], d[3][i]));
     }
     // lanes xc, xc + 16, xc + 32, xc + 48 share a column group
-    const float s0 = col_reduce(sxv.x), s1 = col_reduce(sxv.y), s2 = col_reduce(sxv.z), s3 = col_reduce(sxv.w);
+    float sx[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sx[i] = col_reduce(d[0][i] + d[1][i] + d[2][i] + d[3][i]);
     if (g == 0) {
       float* rs = red + 3 * H0 + 4 * xc;
-      atomicAdd(rs + 0, s0);
-      atomicAdd(rs + 1, s1);
-      atomicAdd(rs + 2, s2);
-      atomicAdd(rs + 3, s3);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) atomicAdd(rs + i, sx[i]);
     }
     if (blockIdx.x == 0) {  // inv0 * gamma0 and the shift row for k_reduce_adam
       if (threadIdx.x < H0) T.k0s[threadIdx.x] = c0[H0 + threadIdx.x];
@@ -1476,26 +1479,38 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   __syncthreads();
   TT_STAMP(3, 4);
 
-  // ---- phase 4: P | Q = [dY0 | Zh0]^T X' over the tile's rows: wave w owns
-  // channels 16 (w & 3) .. +15 of P (w < 4) or Q, every column tile.  Slab
-  // layout [64][kp/16][P 16 | Q 16]: k_reduce_adam's lanes for 16 columns of
-  // P and the same 16 of Q read one contiguous 128 B
+  // ---- phase 4: P | Q = [dY0 | Zh0]^T X' over the tile's rows (bf16x3,
+  // K = rows in 32-row steps): wave w owns channels 16 (w & 3) .. +15 of P
+  // (w < 4) or Q, every column tile.  Slab layout [64][kp/16][P 16 | Q 16]:
+  // k_reduce_adam's lanes for 16 columns of P and the same 16 of Q read one
+  // contiguous 128 B
   {
-    const float* As = smem + (w < 4 ? L::Yr : L::Zr) + 16 * (w & 3);
+    const uint16_t* hs = reinterpret_cast<const uint16_t*>(smem);
+    const uint16_t* Ai = hs + (w < 4 ? L::IY : L::IZ);
+    const uint16_t* Bi = hs + L::IX;
     const int kp = T.kp, KT = kp / 16;
+    const int ca = 16 * (w & 3) + r;
     const int so = (int)T.so_W0 + 16 * (w & 3) * 2 * kp + (w < 4 ? 0 : 16);
-    if (KT == 4) {
-      f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-      strip_gemm_tn<4>(As, LDR, smem + L::Xr, LDR, R, acc);
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) store_tile_rm_wt(slab, so + 32 * q, 2 * kp, acc[q]);
-    } else {
-      for (int kt = 0; kt < KT; ++kt) {
-        f32x4 acc[1] = {zero4()};
-        strip_gemm_tn<1>(As, LDR, smem + L::Xr + 16 * kt, LDR, R, acc);
-        store_tile_rm_wt(slab, so + 32 * kt, 2 * kp, acc[0]);
+    for (int kk = 0; kk < R / 32; ++kk) {
+      const int k0 = 32 * kk + 8 * g;
+      bf16x8 af[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) af[p] = *reinterpret_cast<const bf16x8*>(Ai + p * L::PL + fold_at(ca, k0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < KT) {
+          bf16x8 bf[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bf[p] = *reinterpret_cast<const bf16x8*>(Bi + p * L::PL + fold_at(16 * j + r, k0));
+          mfma_x3(af, bf, acc[j]);
+        }
       }
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < KT) store_tile_rm_wt(slab, so + 32 * j, 2 * kp, acc[j]);
   }
   if (threadIdx.x < H0) {
     float* fr = T.fr + rep_of_block() * FRW;

@@ -107,6 +107,15 @@ int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out /* TT_NUM_OFFSETS 
 /* BN running stats arena (floats): per tower running_mean0[64] running_var0[64]
  * running_mean1[32] running_var1[32]; num_batches_tracked lives in a separate
  * int64[4] array (firm bn1, firm bn5, ceo bn1, ceo bn5). */
+/* How a training step of this model at this batch size runs (no GPU work):
+ * info[0] = 1 when the BN0 backward is folded into k_bwd_mid (numeric-only
+ * towers, widths % 4 == 0 and <= 64: k_bwd_first is not launched),
+ * info[1] = k_top row tile, info[2] = k_bwd_mid row tile, info[3] = kernels
+ * per tt_train_step (5 or 6; the event slots of tt_train_step_ev are fixed:
+ * l0, l4, top, mid, first, reduce -- slot 4 stays unrecorded when folded).
+ * Replaces nothing in the reference (training.py:44-57 is one autograd
+ * pass); a query for callers that time or trace the step.             */
+int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32_t n_info);
 int64_t tt_buffer_count(const tt_model_desc* d);
 /* Bytes of the workspace for batches of up to max_batch.  Zero it once and
  * keep it with its trainer: its leading region (offsets independent of the

@@ -71,7 +71,7 @@ def kernel_work(nf, nc, D, B, n_params, plan):
         "k_bwd_first": 0 if fold else 2 * B * 64 * (nf + nc),        # dW0
         "k_reduce_adam": 0,
     }
-    w0_slab = (2 * 64 * (kp(nf) + kp(nc)) * 2) if fold else (64 * (nf + nc) + 128)
+    w0_slab = (2 * 64 * (kp(nf) + kp(nc))) if fold else (64 * (nf + nc) + 128)  # P | Q, or dW0 | db0
     by = {
         "k_l0_fwd": B * (nf + nc) * f + 2 * B * 64 * f,
         "k_l4_fwd": 2 * B * 64 * f + 2 * B * 32 * f,

@@ -38,7 +38,8 @@ struct Layout {
   int64_t n;          // parameter count
   int64_t so[2][6];   // slab offsets W0 b0 W4 b4 W8 b8
   int64_t slab_ld;
-  bool fold;          // numeric-only towers, kp <= 64: BN0 backward folded into k_bwd_mid
+  bool fold_ok;       // numeric-only towers, widths % 4 == 0 and <= 64: the BN0 backward can be
+                      // folded into k_bwd_mid (slab W0 range sized for P | Q); Plan::fold decides
 };
 
 static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
@@ -68,15 +69,15 @@ static Layout make_layout(const tt_model_desc* d) {
       off = round_up(off + (int64_t)d->cat_counts[t][j] * d->emb_dim[t], 4);
     }
   const int D = d->latent;
-  L.fold = true;
+  L.fold_ok = true;
   for (int t = 0; t < 2; ++t) {
     const int in = d->n_num[t] + d->n_cat[t] * d->emb_dim[t];
     L.in_dim[t] = in;
     L.kp[t] = (int)round_up(in, 16);
-    L.fold = L.fold && d->n_cat[t] == 0 && in % 4 == 0 && L.kp[t] <= FOLD_MAX_KP;
+    L.fold_ok = L.fold_ok && d->n_cat[t] == 0 && in % 4 == 0 && L.kp[t] <= FOLD_MAX_KP;
   }
 #ifdef TT_NO_FOLD
-  L.fold = false;
+  L.fold_ok = false;
 #endif
   for (int t = 0; t < 2; ++t) {
     const int in = L.in_dim[t];
@@ -88,7 +89,7 @@ static Layout make_layout(const tt_model_desc* d) {
     }
     int64_t so = 0;
     // folded: P and Q partials interleaved [64][kp/16][P 16 | Q 16] in the W0 range
-    L.so[t][0] = so; so += (int64_t)H0 * (L.fold ? 2 * L.kp[t] : in);
+    L.so[t][0] = so; so += (int64_t)H0 * (L.fold_ok ? 2 * L.kp[t] : in);
     L.so[t][1] = so; so += H0;
     L.so[t][2] = so; so += (int64_t)H1 * H0;
     L.so[t][3] = so; so += H1;
@@ -183,6 +184,7 @@ struct Plan {
   int n_tiles;      // 64-row tiles
   int n_tiles_top;  // k_top tiles
   int n_tiles_mid;  // k_bwd_mid tiles (FOLD_ROWS rows when the BN0 backward is folded)
+  bool fold;        // BN0 backward folded into k_bwd_mid_fold (k_bwd_first not launched)
 };
 
 static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P) {
@@ -201,13 +203,16 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   // kernel reads was written earlier in the same step
   P->n_tiles = (int)(padded_rows(B) / ROWS);
   P->n_tiles_top = (int)((P->n_tiles * ROWS) / P->top_rows);
-  P->n_tiles_mid = L.fold ? (int)((P->n_tiles * ROWS) / FOLD_ROWS) : P->n_tiles;
+  // folded only for batches that still give the 128-row kernel >= 64 tiles
+  // per tower: cfg 2 (B = 4096) measured 45.9 us folded vs 42.4 us not
+  P->fold = L.fold_ok && B >= TT_FOLD_MIN_B;
+  P->n_tiles_mid = P->fold ? (int)((P->n_tiles * ROWS) / FOLD_ROWS) : P->n_tiles;
   P->lds_l0 = L0Lds<ROWS>::bytes(kpm);
   P->lds_l4 = L4Lds<ROWS>::bytes;
   const int tl = P->ndt == 4 ? (P->top_rows == 64 ? TopLds<4, 64>::total : TopLds<4, 128>::total)
                              : (P->top_rows == 64 ? TopLds<8, 64>::total : TopLds<8, 128>::total);
   P->lds_top = sizeof(float) * (size_t)tl;
-  P->lds_mid = L.fold ? FoldLds<FOLD_ROWS>::bytes : MidLds<ROWS>::bytes;
+  P->lds_mid = P->fold ? FoldLds<FOLD_ROWS>::bytes : MidLds<ROWS>::bytes;
   P->lds_first = FirstLds<ROWS>::bytes(kpm);
   (void)emb;
   for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first})
@@ -224,7 +229,8 @@ static bool batch_ok(const tt_model_desc* d, const tt_batch* b) {
   return true;
 }
 
-static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, const WsLayout& W, const float* params,
+static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, const WsLayout& W, bool fold,
+                      const float* params,
                       float* buffers, int64_t* nbt, const tt_batch* b, float* ws) {
   std::memset(&a, 0, sizeof(a));
   for (int t = 0; t < 2; ++t) {
@@ -293,12 +299,12 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
     T.fr = ws + W.fr + (int64_t)t * NREP * FRW;
     T.k0s = ws + W.k0s[t];
     T.xsh = ws + W.xsh[t];
-    if (L.fold) {  // the folded k_bwd_mid accumulates gg0 | gbe0 into the fold replicas
+    if (fold) {  // the folded k_bwd_mid accumulates gg0 | gbe0 into the fold replicas
       T.gg0 = T.fr;
       T.gbe0 = T.fr + H0;
     }
   }
-  if (L.fold) {
+  if (fold) {
     a.fr_zero = ws + W.fr;
     a.fr_zero_len = 2 * NREP * FRW;
   }
@@ -349,7 +355,7 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     const int64_t* s = L.slot[t];
     float* bng = ws + W.bng[t];
     // gamma|beta slots are adjacent and unpadded (H0, H1 multiples of 4): same order as a replica
-    if (L.fold) {
+    if (P.fold) {
       float* fr = ws + W.fr + (int64_t)t * NREP * FRW;
       for (int kind = 3; kind <= 4; ++kind) {
         add(s[kind == 3 ? TT_SLOT_W0 : TT_SLOT_B0], kind == 3 ? (int64_t)H0 * L.in_dim[t] : H0, kind, t,
@@ -363,7 +369,9 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
       add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, fr, FRW);
       r.seg[k - 1].keep = 1;  // zeroed by the next step's k_l0_fwd
     } else {
-      add(s[TT_SLOT_W0], s[TT_SLOT_G0] - s[TT_SLOT_W0], 0, t, L.so[t][0], P.n_tiles);
+      // W0 and b0 apart: the slab's W0 range may be sized for the folded P | Q
+      add(s[TT_SLOT_W0], (int64_t)H0 * L.in_dim[t], 0, t, L.so[t][0], P.n_tiles);
+      add(s[TT_SLOT_B0], H0, 0, t, L.so[t][1], P.n_tiles);
       add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, bng, BNG);
     }
     add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles_mid);
@@ -525,10 +533,10 @@ int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32
   Plan P;
   const int rc = make_plan(d, L, batch, &P);
   if (rc) return rc;
-  info[0] = L.fold ? 1 : 0;
+  info[0] = P.fold ? 1 : 0;
   info[1] = P.top_rows;
-  info[2] = L.fold ? FOLD_ROWS : ROWS;
-  info[3] = L.fold ? 5 : 6;
+  info[2] = P.fold ? FOLD_ROWS : ROWS;
+  info[3] = P.fold ? 5 : 6;
   return TT_OK;
 }
 
@@ -554,7 +562,7 @@ static int32_t forward_impl(const tt_model_desc* d, const float* params, float* 
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   StepArgs a;
-  fill_args(a, d, c.L, c.W, params, buffers, nbt, b, w);
+  fill_args(a, d, c.L, c.W, c.P.fold, params, buffers, nbt, b, w);
   a.train = train ? 1 : 0;
   a.update_stats = a.train;
   a.seed = seed;
@@ -599,7 +607,7 @@ static int32_t backward_impl(const tt_model_desc* d, const float* params, const 
   float* w = (float*)ws;
   // running-stat buffers are not touched by backward; pass a dummy-safe pointer
   StepArgs a;
-  fill_args(a, d, c.L, c.W, params, nullptr, nullptr, b, w);
+  fill_args(a, d, c.L, c.W, c.P.fold, params, nullptr, nullptr, b, w);
   a.train = 1;
   a.update_stats = 0;
   a.seed = seed;
@@ -610,7 +618,7 @@ static int32_t backward_impl(const tt_model_desc* d, const float* params, const 
   (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
   for (int t = 0; t < 2; ++t) (void)hipMemsetAsync(w + c.W.bng[t], 0, sizeof(float) * NREP * BNG, s);
   (void)hipMemsetAsync(w + c.W.lsr, 0, sizeof(float) * NREP * LSR, s);
-  if (c.L.fold) (void)hipMemsetAsync(w + c.W.fr, 0, sizeof(float) * 2 * NREP * FRW, s);
+  if (c.P.fold) (void)hipMemsetAsync(w + c.W.fr, 0, sizeof(float) * 2 * NREP * FRW, s);
   launch_top(a, c.P, 2, s);
   launch_mid(a, c.P, s);
   launch_first(a, c.P, s);
@@ -645,7 +653,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   StepArgs a;
-  fill_args(a, d, c.L, c.W, params, buffers, nbt, b, w);
+  fill_args(a, d, c.L, c.W, c.P.fold, params, buffers, nbt, b, w);
   a.train = 1;
   a.update_stats = 1;
   a.seed = seed;

@@ -197,3 +197,65 @@ def test_exchange_timeout_leaves_parameters_and_raises():
         torch.cuda.synchronize()
         L.tt_ar_free(ctypes.c_void_p(regs[1]))
         ex.close()
+
+
+def _ddp_fold_rank(rank, world, port, q):
+    """B = 8192 per rank on the cfg-3 model: the folded BN0 backward
+    (k_bwd_mid_fold + the reduce's P/Q combine, apply_adam = 0) feeding the
+    peer exchange + Adam, vs the oracle's per-shard local-BN DDP step."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CEO_TT_PEER_AR="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching import CEOFirmMatcher, Config
+        from ceo_firm_matching import _native as N
+        from ceo_firm_matching.engine import FusedTrainer
+        from oracle import two_tower as O
+        dev = torch.device("cuda:0")
+        g = load_golden("cfg3")
+        meta = meta_of(g)
+        B = 8192
+        rng = np.random.default_rng(5)  # every rank draws all shards, keeps its own
+        shards = []
+        for _ in range(world):
+            shards.append({
+                "firm_numeric": torch.from_numpy(rng.standard_normal((B, meta["n_firm_numeric"])).astype(np.float32)),
+                "firm_cat": torch.zeros(B, 0, dtype=torch.int64),
+                "ceo_numeric": torch.from_numpy(rng.standard_normal((B, meta["n_ceo_numeric"])).astype(np.float32)),
+                "ceo_cat": torch.zeros(B, 0, dtype=torch.int64),
+                "target": torch.from_numpy(rng.standard_normal((B, 1)).astype(np.float32)),
+                "weights": torch.from_numpy(rng.uniform(1, 10, (B, 1)).astype(np.float32)),
+            })
+        cfg = Config()
+        cfg.LATENT_DIM = int(g["meta/latent"])
+        cfg.DROPOUT_P = 0.0
+        cfg.DEVICE = dev
+        m = CEOFirmMatcher(meta, cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()})
+        m = m.to(dev)
+        assert N.step_plan(m.tt_desc(), B)["folded_bn0_backward"]
+        tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=0, process_group=dist.group.WORLD)
+        assert tr.peer is not None
+        tr.set_data({k: v.to(dev) for k, v in shards[rank].items()})
+        tr.step(None, 0, B)
+        tr.pop_loss_sum()
+        P = {k: torch.from_numpy(v).double() for k, v in sub(g, "init").items() if k in O.param_names(meta)}
+        buf = {k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items() if k in O.buffer_names()}
+        buf = {k: (v if "num_batches" in k else v.double()) for k, v in buf.items()}
+        avg = O.ddp_average_grads(P, buf, shards, p=0.0)
+        O.Adam(P, lr=4e-4).step(P, avg)
+        errs = {k: normwise(p.detach().cpu().double().numpy(), P[k].numpy()) for k, p in m.named_parameters()
+                if not excluded_param(k)}
+        q.put((rank, max(errs.values()), max(errs, key=errs.get)))
+    except Exception as e:
+        q.put((rank, float("inf"), repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_folded_step_on_peer_exchange():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    for rank, err, where in _spawn(_ddp_fold_rank, 2):
+        assert err < 1e-5, (rank, err, where)

@@ -32,7 +32,8 @@ EXPORTED = ("tt_abi_version", "tt_param_count", "tt_param_offsets", "tt_buffer_c
             "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_train_step", "tt_train_step_ev",
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
             "tt_nce_workspace_bytes", "tt_nce_norms", "tt_nce_forward", "tt_nce_loss", "tt_nce_backward",
-            "tt_rank_workspace_bytes", "tt_retrieval_ranks", "tt_step_plan")
+            "tt_rank_workspace_bytes", "tt_retrieval_ranks", "tt_step_plan",
+            "tt_nce_maxes", "tt_nce_forward_lse", "tt_nce_loss_lse", "tt_nce_backward_lse")
 
 
 class NativeLibraryError(RuntimeError):
@@ -110,6 +111,10 @@ def lib() -> ctypes.CDLL:
         "tt_nce_forward": (I32, [P, P, I64, I64, I32, I64, F, P, P, I64, P, P]),
         "tt_nce_loss": (I32, [I64, I64, I32, I64, I64, F, P, I64, P, P, P, P]),
         "tt_nce_backward": (I32, [P, P, I64, I64, I32, I64, I64, F, P, I64, P, P, P]),
+        "tt_nce_maxes": (I32, [P, P, I64, I64, I32, I64, F, P, I64, P, P]),
+        "tt_nce_forward_lse": (I32, [P, P, I64, I64, I32, I64, F, P, P, I64, P, P]),
+        "tt_nce_loss_lse": (I32, [I64, I64, I32, I64, I64, P, I64, P, P, P, P, P]),
+        "tt_nce_backward_lse": (I32, [P, P, I64, I64, I32, I64, I64, F, P, I64, P, P, P]),
         "tt_rank_workspace_bytes": (I64, [I64]),
         "tt_retrieval_ranks": (I32, [P, P, I64, I64, I32, I64, P, I64, P, P]),
         "tt_ar_region_bytes": (I64, [I64]),

@@ -40,12 +40,27 @@ from . import _native as N
 from .config import Config
 from .model import _POISON_WS, CEOFirmMatcher
 
-def _check_status(status: torch.Tensor):
+def _status_bad(status: torch.Tensor) -> bool:
+    """Underflowed softmax sums in the shared-shift pass (host read)."""
+    return int(status.item()) != 0
+
+
+def _check_robust(status: torch.Tensor):
     bad = int(status.item())
     if bad:
-        raise NotImplementedError(
-            f"info_nce_loss: {bad} softmax sums underflowed; the fused kernels share one exponent shift "
-            "(max|f| max|c| / temperature) and expect (near-)L2-normalised projections")
+        raise FloatingPointError(f"info_nce_loss: {bad} non-finite log-sum-exps (inf / nan in the projections)")
+
+
+_F64_WARNED = False
+
+
+def _warn_f64(*xs):
+    global _F64_WARNED
+    if not _F64_WARNED and any(x.dtype == torch.float64 for x in xs):
+        import warnings
+        warnings.warn("info_nce_loss: float64 projections are scored by the fp32-accurate HIP kernels "
+                      "(results and gradients in float64, arithmetic at fp32 accuracy)", RuntimeWarning, stacklevel=3)
+        _F64_WARNED = True
 
 
 def _f32(x: torch.Tensor) -> torch.Tensor:
@@ -100,12 +115,37 @@ class _NCE:
                                    status.data_ptr(), self.st), "tt_nce_loss")
         return loss, status
 
+    # robust (two-exponent) pass: the fallback when loss() reports underflow
+    def maxes(self):
+        col_max = torch.empty(self.n, dtype=torch.float32, device=self.f.device)
+        N.check(self.L.tt_nce_maxes(self.f.data_ptr(), self.c.data_ptr(), self.m, self.n, self.d, self.row0,
+                                    ctypes.c_float(self.tau), self.ws.data_ptr(), self.ws_bytes, col_max.data_ptr(),
+                                    self.st), "tt_nce_maxes")
+        return col_max
+
+    def forward_lse(self, col_max):
+        col_sum = torch.empty(self.n, dtype=torch.float32, device=self.f.device)
+        N.check(self.L.tt_nce_forward_lse(self.f.data_ptr(), self.c.data_ptr(), self.m, self.n, self.d, self.row0,
+                                          ctypes.c_float(self.tau), col_max.data_ptr(), self.ws.data_ptr(),
+                                          self.ws_bytes, col_sum.data_ptr(), self.st), "tt_nce_forward_lse")
+        return col_sum
+
+    def loss_lse(self, col_max, col_sum):
+        loss = torch.zeros(1, dtype=torch.float32, device=self.f.device)
+        status = torch.zeros(1, dtype=torch.int32, device=self.f.device)
+        N.check(self.L.tt_nce_loss_lse(self.m, self.n, self.d, self.row0, self.batch, self.ws.data_ptr(),
+                                       self.ws_bytes, col_max.data_ptr(), col_sum.data_ptr(), loss.data_ptr(),
+                                       status.data_ptr(), self.st), "tt_nce_loss_lse")
+        self.robust = True
+        return loss, status
+
     def backward(self):
         df = torch.empty(self.m, self.d, dtype=torch.float32, device=self.f.device)
         dc = torch.empty(self.n, self.d, dtype=torch.float32, device=self.f.device)
-        N.check(self.L.tt_nce_backward(self.f.data_ptr(), self.c.data_ptr(), self.m, self.n, self.d, self.row0,
-                                       self.batch, ctypes.c_float(self.tau), self.ws.data_ptr(), self.ws_bytes,
-                                       df.data_ptr(), dc.data_ptr(), self.st), "tt_nce_backward")
+        fn = self.L.tt_nce_backward_lse if getattr(self, "robust", False) else self.L.tt_nce_backward
+        N.check(fn(self.f.data_ptr(), self.c.data_ptr(), self.m, self.n, self.d, self.row0,
+                   self.batch, ctypes.c_float(self.tau), self.ws.data_ptr(), self.ws_bytes,
+                   df.data_ptr(), dc.data_ptr(), self.st), "tt_nce_backward")
         return df, dc
 
 
@@ -116,7 +156,10 @@ class _InfoNCEFn(torch.autograd.Function):
         B, d = f32.shape
         h = _NCE(f32, c32, B, B, d, 0, B, float(temperature))
         loss, status = h.loss(h.forward(h.norms()))
-        _check_status(status)
+        if _status_bad(status):  # shared shift underflowed: exact row / column maxima
+            col_max = h.maxes()
+            loss, status = h.loss_lse(col_max, h.forward_lse(col_max))
+            _check_robust(status)
         ctx.h = h
         ctx.dtypes = (f.dtype, c.dtype)
         ctx.d_in = f.shape[1]
@@ -139,6 +182,7 @@ def info_nce_loss(firm_proj: torch.Tensor, ceo_proj: torch.Tensor, temperature: 
     if firm_proj.device.type == "cuda":
         if firm_proj.shape != ceo_proj.shape:
             raise ValueError("info_nce_loss: firm_proj and ceo_proj must have the same shape")
+        _warn_f64(firm_proj, ceo_proj)
         return _InfoNCEFn.apply(firm_proj, ceo_proj, temperature)
     sim_matrix = torch.mm(firm_proj, ceo_proj.t()) / temperature
     labels = torch.arange(B, device=firm_proj.device)
@@ -169,7 +213,15 @@ class _ShardedNCEFn(torch.autograd.Function):
         loss, status = h.loss(col_sum)
         dist.all_reduce(loss, group=group)
         dist.all_reduce(status, group=group)
-        _check_status(status)
+        if _status_bad(status):  # every rank takes the robust pass together
+            col_max = h.maxes()
+            dist.all_reduce(col_max, op=dist.ReduceOp.MAX, group=group)
+            col_sum = h.forward_lse(col_max)
+            dist.all_reduce(col_sum, group=group)
+            loss, status = h.loss_lse(col_max, col_sum)
+            dist.all_reduce(loss, group=group)
+            dist.all_reduce(status, group=group)
+            _check_robust(status)
         ctx.h, ctx.group, ctx.m = h, group, m
         return loss.reshape(())
 

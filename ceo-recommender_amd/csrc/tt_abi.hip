@@ -791,7 +791,7 @@ struct NceLayout {
   int64_t d_pad, pntj;      // grad outputs: columns (D) in 16-tiles
   int64_t split_f, kps_f;   // dF = E' C   (K = n_pad)
   int64_t split_c, kps_c;   // dC = E'^T F (K = m_pad)
-  int64_t E, rowpart, colpart, rowsum, diag, a, b, shift, part, total;  // float offsets
+  int64_t E, rowpart, colpart, rowsum, diag, a, b, shift, part, rmax, cmax, total;  // float offsets
 };
 
 static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
@@ -833,6 +833,8 @@ static NceLayout nce_layout(int64_t m, int64_t n, int d) {
   L.b = take(L.n_pad);
   L.shift = take(1);
   L.part = take(std::max(L.split_f * L.nti, L.split_c * L.ntj) * L.pntj * TILE);
+  L.rmax = take(L.m_pad);  // robust mode: row / column maxima of s
+  L.cmax = take(L.n_pad);
   L.total = off;
   return L;
 }
@@ -846,8 +848,10 @@ static bool nce_args_ok(const float* f, const float* c, int64_t m, int64_t n, in
 static std::once_flag g_nce_attr;
 static void nce_attrs() {
   std::call_once(g_nce_attr, [] {
-    const void* sim[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>, (const void*)k_nce_sim<2>};
-    const void* grad[] = {(const void*)k_nce_dgrad<SRC_E_ROWS>, (const void*)k_nce_dgrad<SRC_E_AS_MK>};
+    const void* sim[] = {(const void*)k_nce_sim<0>, (const void*)k_nce_sim<1>, (const void*)k_nce_sim<2>,
+                         (const void*)k_nce_sim<3>, (const void*)k_nce_sim<4>};
+    const void* grad[] = {(const void*)k_nce_dgrad<SRC_E_ROWS, false>, (const void*)k_nce_dgrad<SRC_E_AS_MK, false>,
+                          (const void*)k_nce_dgrad<SRC_E_ROWS, true>, (const void*)k_nce_dgrad<SRC_E_AS_MK, true>};
     for (const void* k : sim) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_SIM);
     for (const void* k : grad)
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_GRAD);
@@ -938,9 +942,12 @@ int32_t tt_nce_loss(int64_t m, int64_t n, int32_t d, int64_t row0, int64_t batch
   return launch_check();
 }
 
-int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
-                        int64_t batch, float temperature, void* ws, int64_t ws_bytes, float* df, float* dc,
-                        tt_stream_t stream) {
+}  // extern "C"
+
+template <bool LSE>
+static int32_t nce_backward_impl(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                                 int64_t batch, float temperature, void* ws, int64_t ws_bytes, float* df, float* dc,
+                                 tt_stream_t stream) {
   using namespace tt::nce;
   if (!nce_args_ok(f, c, m, n, d, row0) || !ws || !df || !dc || batch < 2 || !(temperature > 0.f))
     return TT_ERR_ARG;
@@ -965,7 +972,7 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.p_nti = L.nti;
     g.p_ntj = L.pntj;
     const dim3 grid((unsigned)(((m + CfgGrad::BM - 1) / CfgGrad::BM) * g.n_blocks_n), (unsigned)L.split_f);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_ROWS>, grid, dim3(CfgGrad::NTH), LDS_GRAD, s, g);
+    hipLaunchKernelGGL((k_nce_dgrad<SRC_E_ROWS, LSE>), grid, dim3(CfgGrad::NTH), LDS_GRAD, s, g);
     const int64_t el = L.nti * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_f, L.nti, L.pntj, m, d, scale, corr, c, n, row0, df);
@@ -984,12 +991,104 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
     g.p_nti = L.ntj;
     g.p_ntj = L.pntj;
     const dim3 grid((unsigned)(((n + CfgGrad::BM - 1) / CfgGrad::BM) * g.n_blocks_n), (unsigned)L.split_c);
-    hipLaunchKernelGGL(k_nce_dgrad<SRC_E_AS_MK>, grid, dim3(CfgGrad::NTH), LDS_GRAD, s, g);
+    hipLaunchKernelGGL((k_nce_dgrad<SRC_E_AS_MK, LSE>), grid, dim3(CfgGrad::NTH), LDS_GRAD, s, g);
     const int64_t el = L.ntj * L.pntj * 64;
     hipLaunchKernelGGL(k_nce_grad_finish, dim3((unsigned)std::min<int64_t>((el + 255) / 256, 8192)), dim3(256), 0,
                        s, w + L.part, L.split_c, L.ntj, L.pntj, n, d, scale, corr, f, m, -row0, dc);
   }
   return launch_check();
+}
+
+extern "C" {
+
+int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                        int64_t batch, float temperature, void* ws, int64_t ws_bytes, float* df, float* dc,
+                        tt_stream_t stream) {
+  return nce_backward_impl<false>(f, c, m, n, d, row0, batch, temperature, ws, ws_bytes, df, dc, stream);
+}
+
+// ---- robust (two-exponent) InfoNCE: the fallback when tt_nce_loss reports underflow
+int32_t tt_nce_maxes(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                     float temperature, void* ws, int64_t ws_bytes, float* col_max, tt_stream_t stream) {
+  using namespace tt::nce;
+  if (!nce_args_ok(f, c, m, n, d, row0) || !ws || !col_max || !(temperature > 0.f)) return TT_ERR_ARG;
+  const NceLayout L = nce_layout(m, n, d);
+  if (L.total * (int64_t)sizeof(float) > ws_bytes) return TT_ERR_WORKSPACE;
+  nce_attrs();
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  GemmArgs g = sim_args(f, c, m, n, d, row0);
+  g.inv_tau = 1.0f / temperature;
+  g.rowpart = w + L.rowpart;
+  g.colpart = w + L.colpart;
+  g.m_pad = L.m_pad;
+  g.n_pad = L.n_pad;
+  hipLaunchKernelGGL(k_nce_sim<3>, dim3((unsigned)(L.n_bm * L.n_bn)), dim3(CfgSim::NTH), LDS_SIM, s, g);
+  const int64_t tot = L.m_pad + L.n_pad;
+  const int nb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_nce_reduce_parts<true>, dim3(nb), dim3(256), 0, s, w + L.rowpart, L.n_rp, L.m_pad,
+                     w + L.colpart, L.n_cp, L.n_pad, w + L.rmax, w + L.cmax);
+  (void)hipMemcpyAsync(col_max, w + L.cmax, sizeof(float) * n, hipMemcpyDeviceToDevice, s);
+  return launch_check();
+}
+
+int32_t tt_nce_forward_lse(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                           float temperature, const float* col_max, void* ws, int64_t ws_bytes, float* col_sum,
+                           tt_stream_t stream) {
+  using namespace tt::nce;
+  if (!nce_args_ok(f, c, m, n, d, row0) || !col_max || !ws || !col_sum || !(temperature > 0.f)) return TT_ERR_ARG;
+  const NceLayout L = nce_layout(m, n, d);
+  if (L.total * (int64_t)sizeof(float) > ws_bytes) return TT_ERR_WORKSPACE;
+  nce_attrs();
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  const float inv_tau = 1.0f / temperature;
+  if (col_max != w + L.cmax)  // the caller's (all-reduced) column maxima
+    (void)hipMemcpyAsync(w + L.cmax, col_max, sizeof(float) * n, hipMemcpyDeviceToDevice, s);
+  hipLaunchKernelGGL(k_nce_diag, dim3((unsigned)((L.nti + 3) / 4)), dim3(256), 0, s, f, c, m, n, d, row0, inv_tau,
+                     w + L.diag);
+  GemmArgs g = sim_args(f, c, m, n, d, row0);
+  g.inv_tau = inv_tau;
+  g.E = w + L.E;
+  g.e_nti = L.nti;
+  g.e_ntj = L.ntj;
+  g.rowpart = w + L.rowpart;
+  g.colpart = w + L.colpart;
+  g.m_pad = L.m_pad;
+  g.n_pad = L.n_pad;
+  g.rmax = w + L.rmax;
+  g.cmax = w + L.cmax;
+  hipLaunchKernelGGL(k_nce_sim<4>, dim3((unsigned)(L.n_bm * L.n_bn)), dim3(CfgSim::NTH), LDS_SIM, s, g);
+  const int64_t tot = L.m_pad + L.n_pad;
+  const int nb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_nce_reduce_parts<false>, dim3(nb), dim3(256), 0, s, w + L.rowpart, L.n_rp, L.m_pad,
+                     w + L.colpart, L.n_cp, L.n_pad, w + L.rowsum, w + L.b);
+  (void)hipMemcpyAsync(col_sum, w + L.b, sizeof(float) * n, hipMemcpyDeviceToDevice, s);
+  return launch_check();
+}
+
+int32_t tt_nce_loss_lse(int64_t m, int64_t n, int32_t d, int64_t row0, int64_t batch, void* ws, int64_t ws_bytes,
+                        const float* col_max, const float* col_sum, float* loss, int32_t* status,
+                        tt_stream_t stream) {
+  using namespace tt::nce;
+  if (m < 1 || n < 1 || d < 4 || !ws || !col_max || !col_sum || !loss || batch < 2 || row0 < 0 || row0 + m > n)
+    return TT_ERR_ARG;
+  const NceLayout L = nce_layout(m, n, d);
+  if (L.total * (int64_t)sizeof(float) > ws_bytes) return TT_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  const int64_t tot = L.m_pad + L.n_pad;
+  const int nb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_nce_loss_lse, dim3(nb), dim3(256), 0, s, w + L.rowsum, w + L.rmax, col_sum, col_max,
+                     w + L.diag, m, L.m_pad, n, L.n_pad, row0, (float)(0.5 / (double)batch), w + L.a, w + L.b, loss,
+                     status);
+  return launch_check();
+}
+
+int32_t tt_nce_backward_lse(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                            int64_t batch, float temperature, void* ws, int64_t ws_bytes, float* df, float* dc,
+                            tt_stream_t stream) {
+  return nce_backward_impl<true>(f, c, m, n, d, row0, batch, temperature, ws, ws_bytes, df, dc, stream);
 }
 
 int64_t tt_rank_workspace_bytes(int64_t m) {

@@ -21,6 +21,14 @@
 // different ranks simply add).  L2-normalised inputs give shift = 1/tau and
 // every term >= exp(-2/tau); sums that still underflow (far-from-normalised
 // inputs) are counted in a status word instead of silently returning inf.
+//
+// Robust mode (the caller's fallback when that status is set: temperatures
+// far below 0.03 on normalised inputs, or unnormalised projections): exact
+// per-row and per-column maxima first (k_nce_sim<3>), then row sums of
+// exp(s - rowmax_i) and column sums of exp(s - colmax_j) -- two exponentials
+// per element -- with the logits s themselves kept for the backward
+// (k_nce_sim<4>); the backward stages E' = exp(s - lse_i) + exp(s - lse_j)
+// from the row / column log-sum-exps (k_nce_dgrad<SA, true>).
 #include "tt_common.h"
 
 namespace tt {
@@ -128,8 +136,8 @@ struct Opnd {
   int64_t mdim;    // extent along m (rows of the output side)
   int64_t kdim;    // extent along k
   int64_t nti, ntj;  // E tile grid (SRC_E_*)
-  const float* a;  // E row scale (1/rowsum_i, padded)  (SRC_E_*)
-  const float* b;  // E col scale (1/colsum_j, padded)
+  const float* a;  // E row scale (1/rowsum_i, padded)  (SRC_E_*); robust mode: row log-sum-exp
+  const float* b;  // E col scale (1/colsum_j, padded);  robust mode: column log-sum-exp
 };
 
 struct GemmArgs {
@@ -156,6 +164,9 @@ struct GemmArgs {
   float margin;
   uint64_t* semi_part;  // [N / WN parts][M_pad] min key over semi-hard negatives
   uint64_t* all_part;   // [N / WN parts][M_pad] min key over all negatives
+  // robust mode (MODE 4): exact row maxima [M_pad] and column maxima [N_pad] of s
+  const float* rmax;
+  const float* cmax;
 };
 
 // Orderable 64-bit key of a distance and its column: the float bits mapped
@@ -185,9 +196,38 @@ __device__ __forceinline__ uint64_t row_min16(uint64_t v) {
   return v;
 }
 
+// max over the 16 lanes of a row group / over the 4 row groups of a column
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  return v;
+}
+__device__ __forceinline__ float col_max4(float v) {
+  unsigned u = __float_as_uint(v);
+  auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  unsigned lo = p[0], hi = p[1];
+  v = fmaxf(__uint_as_float(lo), __uint_as_float(hi));
+  u = __float_as_uint(v);
+  auto p2 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  lo = p2[0];
+  hi = p2[1];
+  return fmaxf(__uint_as_float(lo), __uint_as_float(hi));
+}
+
 // ---- global -> registers (4 float4 per thread per operand per K chunk) ----
 // (ROWS x BK floats per operand tile, NT threads: ROWS * 8 / NT float4 each)
-template <int S, int ROWS, int NT>
+// E' staging: default x (a_i + b_j) with a, b the reciprocal row / column
+// sums of E = exp(s - shift); robust (LSE) mode exp(x - a_i) + exp(x - b_j)
+// with x = s and a, b the row / column log-sum-exps (0 outside the tiles).
+template <bool LSE>
+__device__ __forceinline__ float ep(float x, float ai, float bj, bool ok) {
+  if constexpr (LSE) return ok ? __expf(x - ai) + __expf(x - bj) : 0.f;
+  else return x * (ai + bj);
+}
+
+template <int S, int ROWS, int NT, bool LSE = false>
 __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0, float4 (&v)[ROWS * 8 / NT]) {
   constexpr int NQ = ROWS * 8 / NT;
   if constexpr (S == SRC_MK) {  // tile ROWS x BK from G[m][k]: 4 k-octets (2 float4) per row
@@ -234,7 +274,8 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
           f32x4, buf_f32x4(rs, ok ? (uint32_t)(((tm * o.ntj + tk) * TILE + ln * 4) * 4) : BUF_OOB)));
       const float ai = buf_f32(ra, ok ? (uint32_t)((ti * 16 + 4 * (ln >> 4) + (ln & 3)) * 4) : BUF_OOB);
       const float4 bj = buf_f32x4(rb, ok ? (uint32_t)((tj * 16 + (ln & 12)) * 4) : BUF_OOB);
-      v[q] = make_float4(x[0] * (ai + bj.x), x[1] * (ai + bj.y), x[2] * (ai + bj.z), x[3] * (ai + bj.w));
+      v[q] = make_float4(ep<LSE>(x[0], ai, bj.x, ok), ep<LSE>(x[1], ai, bj.y, ok), ep<LSE>(x[2], ai, bj.z, ok),
+                         ep<LSE>(x[3], ai, bj.w, ok));
     }
   } else if constexpr (S == SRC_E_AS_MK) {  // E tiles as [m = j][k = i]: ROWS/16 j-tiles x 2 i-tiles
     const int64_t tj0 = m0 >> 4, ti0 = k0 >> 4;
@@ -251,7 +292,8 @@ __device__ __forceinline__ void load_opnd(const Opnd& o, int64_t m0, int64_t k0,
       const float4 x = buf_f32x4(rs, ok ? (uint32_t)(((tk * o.ntj + tm) * TILE + ln * 4) * 4) : BUF_OOB);
       const float4 ai = buf_f32x4(ra, ok ? (uint32_t)((ti * 16 + 4 * (ln >> 4)) * 4) : BUF_OOB);
       const float bj = buf_f32(rb, ok ? (uint32_t)((tj * 16 + (ln & 15)) * 4) : BUF_OOB);
-      v[q] = make_float4(x.x * (ai.x + bj), x.y * (ai.y + bj), x.z * (ai.z + bj), x.w * (ai.w + bj));
+      v[q] = make_float4(ep<LSE>(x.x, ai.x, bj, ok), ep<LSE>(x.y, ai.y, bj, ok), ep<LSE>(x.z, ai.z, bj, ok),
+                         ep<LSE>(x.w, ai.w, bj, ok));
     }
   }
 }
@@ -313,7 +355,7 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* L, int plane, int m, int 
 // Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T.  One LDS
 // stage; the next chunk's global loads are in flight during the MFMAs of the
 // current one.
-template <int SA, int SB, class C>
+template <int SA, int SB, class C, bool LSE = false>
 __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
                                           uint16_t* smem, f32x4 (&acc)[TM][C::TN]) {
   constexpr int NT = C::NTH, BM_ = C::BM, BN = C::BN, TN = C::TN, WN = C::WN;
@@ -329,7 +371,7 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
   constexpr bool SWZ = SA == SRC_MK && SB == SRC_MK;
   uint16_t* As = smem;
   uint16_t* Bs = smem + Lay<SWZ, BM_>::OPND;
-  load_opnd<SA, BM_, NT>(g_.A, m0, kb, va);
+  load_opnd<SA, BM_, NT, LSE>(g_.A, m0, kb, va);
   load_opnd<SB, BN, NT>(g_.B, n0, kb, vb);
   for (int c = 0; c < nch; ++c) {
     __syncthreads();  // the previous chunk's fragments have been read
@@ -337,7 +379,7 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
     store_opnd<SB, SWZ, BN, NT>(Bs, vb);
     __syncthreads();
     if (c + 1 < nch) {
-      load_opnd<SA, BM_, NT>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
+      load_opnd<SA, BM_, NT, LSE>(g_.A, m0, kb + (int64_t)(c + 1) * BK, va);
       load_opnd<SB, BN, NT>(g_.B, n0, kb + (int64_t)(c + 1) * BK, vb);
     }
     bf16x8 a[TM][NPL];
@@ -499,6 +541,70 @@ __global__ __launch_bounds__(CfgSim::NTH) void k_nce_sim(GemmArgs a) {
       const int64_t gj = n0 + wn * WN + 16 * j + r;
       if (g == 0 && gj < a.n_pad) a.colpart[cpart * a.n_pad + gj] = v;
     }
+  } else if constexpr (MODE == 3 || MODE == 4) {
+    // robust InfoNCE.  MODE 3: per-wave row / column maxima of s -> rowpart /
+    // colpart.  MODE 4: row sums of exp(s - rmax_i), column sums of
+    // exp(s - cmax_j) -> rowpart / colpart, and s itself (-inf outside the
+    // matrix) into the E tiles for the backward.
+    constexpr bool MX = MODE == 3;
+    const float init = MX ? -INFINITY : 0.f;
+    float rs[TM][4];
+    float cs[TN];
+    float cmx[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] = init;
+      const int64_t gj = n0 + wn * WN + 16 * j + r;
+      cmx[j] = MX ? 0.f : a.cmax[gj < a.n_pad ? gj : 0];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int64_t ti = (m0 + wm * WM + 16 * i) / 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        rs[i][q] = init;
+        const int64_t gi = ti * 16 + 4 * g + q;
+        const float rmx = MX ? 0.f : a.rmax[gi < a.m_pad ? gi : 0];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int64_t gj = (n0 + wn * WN + 16 * j) + r;
+          const bool in = gi < a.M && gj < a.N;
+          const float sv = acc[i][j][q] * a.inv_tau;
+          if constexpr (MX) {
+            rs[i][q] = in ? fmaxf(rs[i][q], sv) : rs[i][q];
+            cs[j] = in ? fmaxf(cs[j], sv) : cs[j];
+          } else {
+            rs[i][q] += in ? __expf(sv - rmx) : 0.f;
+            cs[j] += in ? __expf(sv - cmx[j]) : 0.f;
+            acc[i][j][q] = in ? sv : -INFINITY;
+          }
+        }
+      }
+      if constexpr (!MX) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int64_t tj = (n0 + wn * WN + 16 * j) / 16;
+          if (ti < a.e_nti && tj < a.e_ntj)
+            __builtin_nontemporal_store(acc[i][j], reinterpret_cast<f32x4*>(a.E + (ti * a.e_ntj + tj) * TILE) + l);
+        }
+      }
+    }
+    const int64_t rpart = bn * NWN + wn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v = MX ? row_max16(rs[i][q]) : row_reduce16(rs[i][q]);
+        const int64_t gi = m0 + wm * WM + 16 * i + 4 * g + q;
+        if (r == 0 && gi < a.m_pad) a.rowpart[rpart * a.m_pad + gi] = v;
+      }
+    const int64_t cpart = bm * NWM + wm;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float v = MX ? col_max4(cs[j]) : col_reduce(cs[j]);
+      const int64_t gj = n0 + wn * WN + 16 * j + r;
+      if (g == 0 && gj < a.n_pad) a.colpart[cpart * a.n_pad + gj] = v;
+    }
   } else if constexpr (MODE == 2) {
     // semi-hard triplet mining (contrastive.py:163-190): dist = 1 - sim in
     // fp32 as the reference rounds it; per row the smallest semi-hard
@@ -602,7 +708,7 @@ __global__ __launch_bounds__(256) void k_nce_diag(const float* __restrict__ F, c
 // k_nce_dgrad: split-K partial of  E'^(T) X  (dF: E' C, dC: E'^T F) into
 // accumulator-layout tiles part[split][ti][tj][256]
 // ---------------------------------------------------------------------------
-template <int SA>
+template <int SA, bool LSE>
 __global__ __launch_bounds__(CfgGrad::NTH) void k_nce_dgrad(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   using C = CfgGrad;
@@ -615,7 +721,7 @@ __global__ __launch_bounds__(CfgGrad::NTH) void k_nce_dgrad(GemmArgs a) {
   const int64_t kb = split * a.k_per_split;
   const int64_t ke = min(kb + a.k_per_split, a.A.kdim);
   f32x4 acc[TM][TN];
-  gemm_loop<SA, SRC_KROWS, C>(a, m0, n0, kb, ke, smem, acc);
+  gemm_loop<SA, SRC_KROWS, C, LSE>(a, m0, n0, kb, ke, smem, acc);
   const int w = wave_id(), l = lane_id();
   const int wm = w / NWN, wn = w % NWN;
 #pragma unroll
@@ -725,6 +831,62 @@ __global__ __launch_bounds__(256) void k_nce_loss(const float* __restrict__ rows
       const int64_t j = e - m_pad;
       b[j] = j < n ? 1.f / colsum[j] : 0.f;
       bad = j < n && !(colsum[j] >= SUM_MIN);
+    }
+    if (bad && status) atomicAdd(status, 1);
+  }
+  acc = wave_reduce(acc);
+  if (lane_id() == 0) red[wave_id()] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss, (red[0] + red[1] + red[2] + red[3]) * inv_2b);
+}
+
+// robust mode: fixed-order max (MX) or sum of the per-wave partials, as k_nce_sums
+template <bool MX>
+__global__ __launch_bounds__(256) void k_nce_reduce_parts(const float* __restrict__ rowpart, int64_t n_rp,
+                                                          int64_t m_pad, const float* __restrict__ colpart,
+                                                          int64_t n_cp, int64_t n_pad, float* __restrict__ rowv,
+                                                          float* __restrict__ colv) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m_pad + n_pad;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float s = MX ? -INFINITY : 0.f;
+    if (e < m_pad) {
+      for (int64_t p = 0; p < n_rp; ++p) s = MX ? fmaxf(s, rowpart[p * m_pad + e]) : s + rowpart[p * m_pad + e];
+      rowv[e] = s;
+    } else {
+      const int64_t j = e - m_pad;
+      for (int64_t p = 0; p < n_cp; ++p) s = MX ? fmaxf(s, colpart[p * n_pad + j]) : s + colpart[p * n_pad + j];
+      colv[j] = s;
+    }
+  }
+}
+
+// robust loss: a_i = rmax_i + log rowsum_i, b_j = cmax_j + log colsum_j (the
+// log-sum-exps; +inf outside the matrix, where E' must vanish), loss +=
+// (a_i - s_ii) + (b_{row0+i} - s_ii) over this shard's rows, / (2 B).  Every
+// sum is >= 1 (its max term is exp(0)), so *status counts only non-finite ones.
+__global__ __launch_bounds__(256) void k_nce_loss_lse(const float* __restrict__ rowsum, const float* __restrict__ rmax,
+                                                      const float* __restrict__ colsum, const float* __restrict__ cmax,
+                                                      const float* __restrict__ diag, int64_t m, int64_t m_pad,
+                                                      int64_t n, int64_t n_pad, int64_t row0, float inv_2b,
+                                                      float* __restrict__ a, float* __restrict__ b, float* loss,
+                                                      int* status) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m_pad + n_pad;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    bool bad = false;
+    if (e < m_pad) {
+      const float li = e < m ? rmax[e] + logf(rowsum[e]) : INFINITY;
+      a[e] = li;
+      if (e < m) {
+        const float si = diag[e];  // s_ii (k_nce_diag scaled it by 1 / tau)
+        const float lj = cmax[row0 + e] + logf(colsum[row0 + e]);
+        acc += (li - si) + (lj - si);
+        bad = !isfinite(li) || !isfinite(lj);
+      }
+    } else {
+      const int64_t j = e - m_pad;
+      b[j] = j < n ? cmax[j] + logf(colsum[j]) : INFINITY;
     }
     if (bad && status) atomicAdd(status, 1);
   }

@@ -225,6 +225,32 @@ int32_t tt_nce_backward(const float* f, const float* c, int64_t m, int64_t n, in
                         int64_t row0, int64_t batch, float temperature, void* ws,
                         int64_t ws_bytes, float* df, float* dc, tt_stream_t stream);
 
+/* Robust InfoNCE -- the same loss and gradients when tt_nce_loss reports
+ * underflow (temperature far below 0.03 on L2-normalised rows, or
+ * unnormalised projections: contrastive.py:102-138 computes those too).
+ * Exact per-row / per-column maxima replace the shared shift, so every sum
+ * holds its exp(0) term and cannot underflow; two exponentials per element.
+ *   5. tt_nce_maxes      : row maxima of S (ws) and col_max[n] over these m
+ *      rows (all-reduce MAX across row shards);
+ *   6. tt_nce_forward_lse: with the global col_max: row sums of
+ *      exp(s - rowmax), col_sum[n] of exp(s - colmax) over these rows
+ *      (all-reduce SUM), S kept in ws for the backward;
+ *   7. tt_nce_loss_lse   : loss += this shard's share; *status counts
+ *      non-finite log-sum-exps (inf / nan inputs);
+ *   8. tt_nce_backward_lse: df, dc as tt_nce_backward.
+ * Same workspace as the default path (tt_nce_workspace_bytes).            */
+int32_t tt_nce_maxes(const float* f, const float* c, int64_t m, int64_t n, int32_t d, int64_t row0,
+                     float temperature, void* ws, int64_t ws_bytes, float* col_max, tt_stream_t stream);
+int32_t tt_nce_forward_lse(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                           int64_t row0, float temperature, const float* col_max, void* ws,
+                           int64_t ws_bytes, float* col_sum, tt_stream_t stream);
+int32_t tt_nce_loss_lse(int64_t m, int64_t n, int32_t d, int64_t row0, int64_t batch, void* ws,
+                        int64_t ws_bytes, const float* col_max, const float* col_sum, float* loss,
+                        int32_t* status, tt_stream_t stream);
+int32_t tt_nce_backward_lse(const float* f, const float* c, int64_t m, int64_t n, int32_t d,
+                            int64_t row0, int64_t batch, float temperature, void* ws,
+                            int64_t ws_bytes, float* df, float* dc, tt_stream_t stream);
+
 /* compute_retrieval_metrics (contrastive.py:275-332): for firm rows F [m, d]
  * (global rows row0..) against all n ceo rows C, ranks[i] = 1 + #{j != row0+i :
  * f_i.c_j > f_i.c_{row0+i}} -- the rank of the true match under a descending

@@ -87,16 +87,50 @@ def test_info_nce_row_shards_compose():
     assert normwise(dc.cpu().numpy(), rdc.numpy()) < TOL
 
 
-def test_info_nce_rejects_underflowing_inputs():
-    """Far-from-normalised inputs whose softmax sums underflow the shared
-    exponent shift are reported, never returned as inf/nan."""
+def test_info_nce_robust_row_shards_compose():
+    """The robust pass's sharded decomposition (per-shard row maxima, MAX of
+    the column maxima, SUM of the shifted column sums, per-shard losses and
+    dC) reproduces the full loss at a temperature the shared shift cannot
+    serve -- the collectives info_nce_loss_sharded runs in its fallback."""
+    from ceo_firm_matching.contrastive import _NCE
     dev = _dev()
-    from ceo_firm_matching.contrastive import info_nce_loss
+    gen = torch.Generator().manual_seed(4)
+    B, D, W, tau = 1536, 64, 3, 0.004
+    f = torch.nn.functional.normalize(torch.randn(B, D, generator=gen), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(B, D, generator=gen) + 0.5 * f, dim=1)
+    fd, cd = f.to(dev), c.to(dev)
+    m = B // W
+    hs = [_NCE(fd[r * m:(r + 1) * m].contiguous(), cd, m, B, D, r * m, B, tau) for r in range(W)]
+    cmax = torch.stack([h.maxes() for h in hs]).max(dim=0).values
+    col = sum(h.forward_lse(cmax) for h in hs)
+    parts = [h.loss_lse(cmax, col) for h in hs]
+    assert sum(int(st.item()) for _, st in parts) == 0
+    loss = sum(lo for lo, _ in parts)
+    grads = [h.backward() for h in hs]
+    df = torch.cat([g_[0] for g_ in grads])
+    dc = sum(g_[1] for g_ in grads)
+    rl, rdf, rdc = OC.info_nce(f.double(), c.double(), tau)
+    l32, df32, dc32 = OC.info_nce(f, c, tau)
+    assert abs(float(loss) - float(rl)) <= max(TOL * abs(float(rl)), 10 * abs(float(l32) - float(rl)))
+    for got, ref, r32 in ((df, rdf, df32), (dc, rdc, dc32)):
+        assert normwise(got.cpu().numpy(), ref.numpy()) <= max(TOL, 10 * normwise(r32.double().numpy(), ref.numpy()))
+
+
+def test_info_nce_one_long_row_vs_oracle():
+    """One row 40x longer than the rest: the shared shift (40/tau) underflows
+    every other row's sum; the robust pass returns the reference's finite
+    loss and gradients (was: NotImplementedError)."""
+    dev = _dev()
     gen = torch.Generator().manual_seed(1)
     f = torch.nn.functional.normalize(torch.randn(64, 32, generator=gen), dim=1)
-    f[0] *= 40.0  # one long row: shift = 40/tau, the other rows' sums underflow
-    with pytest.raises(NotImplementedError):
-        info_nce_loss(f.to(dev), f.to(dev).clone())
+    f[0] *= 40.0
+    c = f.clone()
+    loss, df, dc = _nce(f.to(dev), c.to(dev))
+    rl, rdf, rdc = OC.info_nce(f.double(), c.double(), 0.07)
+    l32, df32, dc32 = OC.info_nce(f, c, 0.07)
+    assert abs(float(loss.detach()) - float(rl)) <= max(TOL * abs(float(rl)), 10 * abs(float(l32) - float(rl)))
+    for got, ref, r32 in ((df, rdf, df32), (dc, rdc, dc32)):
+        assert normwise(got.cpu().numpy(), ref.numpy()) <= max(TOL, 10 * normwise(r32.double().numpy(), ref.numpy()))
 
 
 def test_retrieval_golden_metrics():
@@ -333,3 +367,55 @@ def test_info_nce_full_cfg5_vs_fp64():
     for got, ref in ((df, rdf), (dc, rdc)):
         err = float((got.double() - ref).abs().max() / ref.abs().max())
         assert err < TOL, err
+
+
+@pytest.mark.parametrize("kind,tau,B,D", [("norm", 0.004, 300, 64), ("norm", 0.005, 1030, 128),
+                                         ("raw", 0.07, 517, 36), ("raw", 0.07, 64, 256)])
+def test_info_nce_underflow_falls_back_to_robust_pass(kind, tau, B, D):
+    """Inputs the shared exponent shift cannot serve (L2-normalised rows at a
+    temperature far below 0.03; unnormalised projections, |f| |c| / tau in
+    the hundreds): the shared-shift pass reports underflowed sums, and
+    info_nce_loss recomputes with exact row / column maxima (tt_nce_maxes,
+    tt_nce_forward_lse, tt_nce_loss_lse, tt_nce_backward_lse).  Loss and
+    gradients vs the fp64 oracle; logits this large carry fp32 rounding of
+    |s| * 2^-24 into every softmax, so the bound is 1e-5 normwise or 10x the
+    fp32 oracle's own error, whichever is larger."""
+    from ceo_firm_matching.contrastive import _NCE
+    dev = _dev()
+    gen = torch.Generator().manual_seed(B * 7 + D)
+    f = torch.randn(B, D, generator=gen)
+    c = torch.randn(B, D, generator=gen) + 0.5 * f
+    if kind == "norm":
+        f, c = torch.nn.functional.normalize(f, dim=1), torch.nn.functional.normalize(c, dim=1)
+    else:
+        f, c = 3.0 * f, 3.0 * c
+    # the default pass does underflow on these inputs (so the fallback runs)
+    fd, cd = f.to(dev).contiguous(), c.to(dev).contiguous()
+    h = _NCE(fd, cd, B, B, D, 0, B, tau)
+    _, status = h.loss(h.forward(h.norms()))
+    assert int(status.item()) > 0
+    loss, df, dc = _nce(fd, cd, tau)
+    rl, rdf, rdc = OC.info_nce(f.double(), c.double(), tau)
+    l32, df32, dc32 = OC.info_nce(f, c, tau)
+    lerr = abs(float(loss.detach()) - float(rl))
+    assert np.isfinite(float(loss.detach()))
+    assert lerr <= max(TOL * abs(float(rl)), 10 * abs(float(l32) - float(rl))), (float(loss), float(rl), float(l32))
+    for got, ref, r32 in ((df, rdf, df32), (dc, rdc, dc32)):
+        err = normwise(got.cpu().numpy(), ref.numpy())
+        err32 = normwise(r32.double().numpy(), ref.numpy())
+        assert err <= max(TOL, 10 * err32), (err, err32)
+
+
+def test_info_nce_float64_inputs_warn_and_return_float64():
+    from ceo_firm_matching import contrastive as CT
+    dev = _dev()
+    gen = torch.Generator().manual_seed(11)
+    f = torch.nn.functional.normalize(torch.randn(64, 32, generator=gen, dtype=torch.float64), dim=1)
+    c = torch.nn.functional.normalize(torch.randn(64, 32, generator=gen, dtype=torch.float64), dim=1)
+    CT._F64_WARNED = False
+    with pytest.warns(RuntimeWarning, match="float64"):
+        loss, df, dc = _nce(f.to(dev), c.to(dev))
+    assert loss.dtype == torch.float64 and df.dtype == torch.float64
+    rl, rdf, _ = OC.info_nce(f, c, 0.07)
+    assert abs(float(loss.detach()) - float(rl)) <= TOL * abs(float(rl))
+    assert normwise(df.cpu().numpy(), rdf.numpy()) < TOL

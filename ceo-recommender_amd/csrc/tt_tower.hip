@@ -1245,6 +1245,7 @@ struct FoldLds {
   static constexpr int IY = 0, IZ = img, IX = 2 * img;
   static constexpr int imgs_f = 3 * img / 2;     // floats
   static_assert(imgs_f >= dead, "images cover the dead region");
+  static_assert(IX / 2 >= dead, "X' image clear of the phase-2 operands (written during phase 2)");
   static constexpr int db4 = imgs_f;             // [32]
   static constexpr int c1 = db4 + H1;            // k1 mb mg mean1 inv1 [5][32]
   static constexpr int c0 = c1 + 5 * H1;         // mean0 alpha0 beta0 inv0 [4][64]
@@ -1256,8 +1257,12 @@ struct FoldLds {
   static_assert(R == 128, "16 chunks of 8 rows per image row: the swizzle covers a whole row");
 };
 
-// bf16 offset of (row c, contraction index k) in a FoldLds image plane
-__device__ __forceinline__ int fold_at(int c, int k) { return c * 128 + ((((k >> 3) ^ c) & 15) << 3) + (k & 7); }
+// bf16 offset of (row c, contraction index k) in a FoldLds image plane; the
+// chunk swizzle folds in c >> 4 so the X' writes (rows 4 xc + i for 16 lanes
+// xc) land on 16 distinct chunks as well as the fragment reads (16 rows)
+__device__ __forceinline__ int fold_at(int c, int k) {
+  return c * 128 + ((((k >> 3) ^ c ^ (c >> 4)) & 15) << 3) + (k & 7);
+}
 
 template <int R, bool VEC>
 __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
@@ -1423,25 +1428,11 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
       sz[j] += zh0[j][i];
     }
   }
-  cols_to_lds<4>(sg, red);
-  cols_to_lds<4>(sb, red + H0);
-  cols_to_lds<4>(sz, red + 2 * H0);
-  __syncthreads();  // every wave is past dW4 (A0T) and dA0 (W4s, dZT)
-  TT_STAMP(3, 3);
-
-  // ---- phase 3: bf16x3 images of dY0, Zh0 (from the accumulator layout:
-  // channel 16j + r, rows 16w + 4g .. +3) and X' (columns 4xc .. +3 of rows
-  // xr0 .. +3); the images overwrite the dead f32 region
+  // X' image (clear of W4s|dZT|A0T) and its column sums while the GEMMs above drain
+  const bool cok = xc < ((T.n_num + 3) >> 2);
   {
     uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = 16 * j + r, o = fold_at(c, 16 * w + 4 * g);
-      put_planes4(hs + L::IY + o, L::PL, make_float4(dyt[j][0], dyt[j][1], dyt[j][2], dyt[j][3]));
-      put_planes4(hs + L::IZ + o, L::PL, make_float4(zh0[j][0], zh0[j][1], zh0[j][2], zh0[j][3]));
-    }
     // X' = X - c on valid rows and columns, 0 elsewhere; column partial sums
-    const bool cok = xc < ((T.n_num + 3) >> 2);
     float d[XK][4];
 #pragma unroll
     for (int k = 0; k < XK; ++k) {
@@ -1466,6 +1457,24 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
       float* rs = red + 3 * H0 + 4 * xc;
 #pragma unroll
       for (int i = 0; i < 4; ++i) atomicAdd(rs + i, sx[i]);
+    }
+  }
+  cols_to_lds<4>(sg, red);
+  cols_to_lds<4>(sb, red + H0);
+  cols_to_lds<4>(sz, red + 2 * H0);
+  __syncthreads();  // every wave is past dW4 (A0T) and dA0 (W4s, dZT)
+  TT_STAMP(3, 3);
+
+  // ---- phase 3: bf16x3 images of dY0, Zh0 (from the accumulator layout:
+  // channel 16j + r, rows 16w + 4g .. +3) over the dead f32 region (X'
+  // went in during phase 2: columns 4xc .. +3 of rows xr0 .. +3)
+  {
+    uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 16 * j + r, o = fold_at(c, 16 * w + 4 * g);
+      put_planes4(hs + L::IY + o, L::PL, make_float4(dyt[j][0], dyt[j][1], dyt[j][2], dyt[j][3]));
+      put_planes4(hs + L::IZ + o, L::PL, make_float4(zh0[j][0], zh0[j][1], zh0[j][2], zh0[j][3]));
     }
     if (blockIdx.x == 0) {  // inv0 * gamma0 and the shift row for k_reduce_adam
       if (threadIdx.x < H0) T.k0s[threadIdx.x] = c0[H0 + threadIdx.x];

@@ -105,6 +105,7 @@ static Layout make_layout(const tt_model_desc* d) {
 struct WsLayout {
   int64_t Z0[2], Z4[2], dY0[2], dY1[2], st0[2], st1[2], sh0[2], sh1[2], fin0[2], fin1[2], bng[2], lsr;
   int64_t fr, k0s[2], xsh[2];  // folded BN0 backward: replicas (both towers), inv0*gamma0, shift row
+  int64_t adam;                // AdamSlot[2]: cached Adam coefficients (k_l0_fwd, k_reduce_adam)
   int64_t tgw;
   int64_t slab[2];
   int64_t gacc;
@@ -140,6 +141,7 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
     W.k0s[t] = take(H0);
     W.xsh[t] = take(FOLD_MAX_KP);
   }
+  W.adam = take(2 * sizeof(AdamSlot) / sizeof(float));
   W.gacc = take(L.n);
   const int64_t rows = padded_rows(max_batch);
   W.n_tiles = (int)(rows / ROWS);
@@ -389,6 +391,11 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     vo = round_up(vo + r.seg[i].vlen, RED_E);
   }
   r.vn = vo;
+  // the first replica segment (BN0 affine: no slab loads) fills the next
+  // step's Adam-coefficient slot
+  r.next_seg = -1;
+  for (int i = 0; i < k && r.next_seg < 0; ++i)
+    if (r.seg[i].kind == 2) r.next_seg = i;
   r.lsr = ws + W.lsr;
   r.n_seg = k;
   r.n_slabs = P.n_tiles;
@@ -481,7 +488,10 @@ static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev
   launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
 static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}) {
-  launch(k_reduce_adam, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
+  if (r.adam_slots)
+    launch(k_reduce_adam<true>, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
+  else
+    launch(k_reduce_adam<false>, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
 }
 
 template <bool EMB>
@@ -659,6 +669,13 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   a.seed = seed;
   a.state = state;
   a.mode = TOP_TRAIN;
+  if (apply_adam) {
+    a.adam_slots = reinterpret_cast<AdamSlot*>(w + c.W.adam);
+    a.adam_lr = hp->lr;
+    a.adam_b1 = hp->beta1;
+    a.adam_b2 = hp->beta2;
+    a.adam_eps = hp->eps;
+  }
   auto ev = [&](int k) {
     Evs e;
     if (events) {
@@ -690,6 +707,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     r.b1 = hp->beta1;
     r.b2 = hp->beta2;
     r.eps = hp->eps;
+    r.adam_slots = a.adam_slots;
     r.state = state;
   }
   launch_reduce(r, s, ev(5));

@@ -344,6 +344,59 @@ struct TowerDev {
 
 enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2, TOP_EMB_FWD = 3, TOP_EMB_BWD = 4 };
 
+// Adam arithmetic of torch 2.10 _single_tensor_adam (training.py:55): bias
+// corrections in double, element math in fp32 (k_reduce_adam, k_adam,
+// k_ar_adam and k_bwd_mid_fold's side reduction)
+struct AdamCoef {
+  float w1, c2, b2, step_size, bc2s, eps;
+};
+
+__device__ __forceinline__ AdamCoef adam_coef(float lr, float b1, float b2, float eps, int64_t t) {
+  const double bc1 = 1.0 - pow((double)b1, (double)t);
+  const double bc2 = 1.0 - pow((double)b2, (double)t);
+  AdamCoef c;
+  c.w1 = (float)(1.0 - (double)b1);
+  c.c2 = (float)(1.0 - (double)b2);
+  c.b2 = b2;
+  c.step_size = (float)((double)lr / bc1);
+  c.bc2s = (float)sqrt(bc2);
+  c.eps = eps;
+  return c;
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamCoef& c) {
+  m = m + c.w1 * (g - m);           // lerp, weight < 0.5 branch
+  v = v * c.b2 + (c.c2 * g) * g;    // mul_ + addcmul_
+  const float denom = sqrtf(v) / c.bc2s + c.eps;
+  p = p + (-c.step_size) * (m / denom);
+}
+
+// Adam coefficients of step t, cached in the workspace at slot t & 1 with
+// the step and hyperparameters they were computed for.  k_reduce_adam of
+// step t reads slot t & 1 and one of its light blocks (a replica segment:
+// no slab loads, slack to spare) computes step t + 1's into the other slot,
+// so the double pow chain is off every critical path; k_l0_fwd recomputes a
+// slot that does not match (first step, a step counter set by the host,
+// changed hyperparameters).  Two slots: the write for t + 1 never races the
+// reads of t.
+struct AdamSlot {
+  int64_t t;
+  float lr, b1, b2, eps;
+  AdamCoef c;
+};
+__device__ __forceinline__ bool adam_slot_ok(const AdamSlot& s, int64_t t, float lr, float b1, float b2,
+                                             float eps) {
+  return s.t == t && s.lr == lr && s.b1 == b1 && s.b2 == b2 && s.eps == eps;
+}
+__device__ __forceinline__ void adam_slot_fill(AdamSlot& s, int64_t t, float lr, float b1, float b2, float eps) {
+  s.c = adam_coef(lr, b1, b2, eps, t);
+  s.lr = lr;
+  s.b1 = b1;
+  s.b2 = b2;
+  s.eps = eps;
+  s.t = t;
+}
+
 struct StepArgs {
   TowerDev tw[2];
   // batch
@@ -372,6 +425,8 @@ struct StepArgs {
   const float* demb;     // [2][B][D] upstream dU | dV (TOP_EMB_BWD)
   float* fr_zero;        // k_l0_fwd zeroes fr_zero[0, fr_zero_len) (both towers' fold replicas)
   int fr_zero_len;
+  AdamSlot* adam_slots;  // non-null: k_l0_fwd makes sure slot t & 1 holds step t's coefficients
+  float adam_lr, adam_b1, adam_b2, adam_eps;
 };
 
 // ---------------------------------------------------------------------------
@@ -616,6 +671,8 @@ struct RedArgs {
   int32_t apply_adam;
   float* p; float* m; float* v;
   float lr, b1, b2, eps;
+  AdamSlot* adam_slots;  // non-null: coefficients from slot t & 1; segment next_seg fills t + 1's
+  int32_t next_seg;
   tt_state* state;
   int64_t step_host;
   float inv_b;           // 1 / batch rows (kinds 3, 4)

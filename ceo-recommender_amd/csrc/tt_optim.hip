@@ -15,30 +15,6 @@
 
 namespace tt {
 
-struct AdamCoef {
-  float w1, c2, b2, step_size, bc2s, eps;
-};
-
-__device__ __forceinline__ AdamCoef adam_coef(float lr, float b1, float b2, float eps, int64_t t) {
-  const double bc1 = 1.0 - pow((double)b1, (double)t);
-  const double bc2 = 1.0 - pow((double)b2, (double)t);
-  AdamCoef c;
-  c.w1 = (float)(1.0 - (double)b1);
-  c.c2 = (float)(1.0 - (double)b2);
-  c.b2 = b2;
-  c.step_size = (float)((double)lr / bc1);
-  c.bc2s = (float)sqrt(bc2);
-  c.eps = eps;
-  return c;
-}
-
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamCoef& c) {
-  m = m + c.w1 * (g - m);           // lerp, weight < 0.5 branch
-  v = v * c.b2 + (c.c2 * g) * g;    // mul_ + addcmul_
-  const float denom = sqrtf(v) / c.bc2s + c.eps;
-  p = p + (-c.step_size) * (m / denom);
-}
-
 // Element space: block b, lane (pg, el) takes virtual element v = b RED_E + el.
 // Every segment's virtual range starts on a block boundary, so the segment
 // (and its kind) is uniform per block: one scalar lookup, no per-lane
@@ -48,6 +24,9 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // el < 16 sums their P partials, el >= 16 the Q partials of the same
 // elements -- so the owner finds both sums in this block's LDS and every lane
 // reads 64 B of one 128-B P|Q row segment.
+// PRE: the step's Adam coefficients come from the workspace cache (AdamSlot,
+// tt_common.h: a fused train step); otherwise the owner lanes compute them.
+template <bool PRE>
 __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedArgs a) {
   static_assert(NREP % RED_G == 0, "kinds 2-4: group pg takes replicas pg, pg + RED_G, ...");
   static_assert(RED_E % 32 == 0, "kind 3 pairs lanes el and el + 16 of a 32-lane group");
@@ -87,7 +66,7 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   // only: the same pow in every wave costs more (11.4 us) than it hides.
   // (The code shape matters: an equivalent lambda form measured 10.1 us.)
   AdamCoef c{};
-  bool coef_done = false;
+  bool coef_done = PRE;
   int ch = 0, kx = 0;  // kinds 3, 4: W0 row / column of this element (kind 4: channel)
   if (kind == 0 || kind == 3) {
     constexpr int UNR = 16;  // slab loads in flight per lane
@@ -126,7 +105,7 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
       float x[U2];
 #pragma unroll
       for (int k = 0; k < U2; ++k) x[k] = ldp(min(pg + k * RED_G, n - 1));
-      if (adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+      if (!PRE && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
       coef_done = true;
 #pragma unroll
       for (int k = 0; k < U2; ++k) acc += (pg + k * RED_G < n) ? x[k] : 0.f;
@@ -135,7 +114,7 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
         float x[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; ++k) x[k] = ldp(min(p0 + k * RED_G, n - 1));
-        if (!coef_done) {
+        if (!PRE && !coef_done) {
           if (adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
           coef_done = true;
         }
@@ -166,7 +145,7 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
     xpart[0][pg][el] = r0;
     xpart[2][pg][el] = r2;
   }
-  if (!coef_done && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+  if (!PRE && !coef_done && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
   part[pg][el] = acc;
   // zero the BN moment sums consumed by this step (one element per thread of
   // the leading blocks); fold the loss replicas (block 0)
@@ -220,13 +199,21 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   a.grad[e] = gsum;
   if (kind == 1) a.gacc[e] = 0.f;
   if (a.apply_adam) {
+    if constexpr (PRE) c = a.adam_slots[t & 1].c;
     adam_elem(pp, pm, pv, gsum, c);
     a.p[e] = pp;
     a.m[e] = pm;
     a.v[e] = pv;
     if (a.state && blockIdx.x == 0 && el == 0) a.state->step_done = t;
+    if constexpr (PRE) {  // a light block caches the next step's coefficients (AdamSlot)
+      if (si == a.next_seg && vb == S.voff && el == 0)
+        adam_slot_fill(a.adam_slots[(t + 1) & 1], t + 1, a.lr, a.b1, a.b2, a.eps);
+    }
   }
 }
+
+template __global__ void k_reduce_adam<true>(RedArgs);
+template __global__ void k_reduce_adam<false>(RedArgs);
 
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ P, const float* __restrict__ G,
                                               float* __restrict__ M, float* __restrict__ V, int64_t n,

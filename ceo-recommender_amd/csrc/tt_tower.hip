@@ -442,6 +442,14 @@ __global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
     *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + threadIdx.x)) = make_float2(a.target[drt], a.weight[drt]);
   }
   if (a.state && blockIdx.x == 0 && t == 0 && threadIdx.x == 0) a.state->step_cur = step;
+  // Adam's coefficients for this step: normally cached by the previous
+  // step's k_reduce_adam (AdamSlot); recomputed here when the slot does not
+  // match (first step, counter or hyperparameters changed by the host)
+  if (a.adam_slots && blockIdx.x == 0 && t == 0 && threadIdx.x == 64) {
+    AdamSlot& sl = a.adam_slots[step & 1];
+    if (!adam_slot_ok(sl, step, a.adam_lr, a.adam_b1, a.adam_b2, a.adam_eps))
+      adam_slot_fill(sl, step, a.adam_lr, a.adam_b1, a.adam_b2, a.adam_eps);
+  }
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H0) atomicAdd(&T.st0[rep_of_block() * 2 * H0 + threadIdx.x], red[threadIdx.x]);

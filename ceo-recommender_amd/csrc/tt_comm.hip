@@ -60,7 +60,7 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
   if (threadIdx.x == 0) ok_s = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
   __syncthreads();
   if (ok_s == 0) return;
-  const int64_t t = a.state ? a.state->step_cur : a.step_host;
+  const int64_t t = a.state ? load_step(a.state, reinterpret_cast<const int64_t*>(a.grad)) : a.step_host;
   const uint64_t epoch = (uint64_t)t;
   const int b = blockIdx.x;
   const int64_t per = (a.n + a.blocks - 1) / a.blocks;

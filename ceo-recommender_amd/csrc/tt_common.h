@@ -435,21 +435,33 @@ struct StepArgs {
 // ---------------------------------------------------------------------------
 #ifdef TT_STAMPS
 extern __device__ uint64_t* g_tt_stamps;
-#define TT_STAMP(kid, slot)                                                                             \
+#define TT_STAMP_T(kid, slot, thr)                                                                      \
   do {                                                                                                  \
-    if (g_tt_stamps && threadIdx.x == 0)                                                                \
+    if (g_tt_stamps && threadIdx.x == (thr))                                                            \
       g_tt_stamps[((uint64_t)(kid) * 2048 + blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] =        \
           __builtin_amdgcn_s_memrealtime();                                                             \
   } while (0)
+#define TT_STAMP(kid, slot) TT_STAMP_T(kid, slot, 0)
 #else
+#define TT_STAMP_T(kid, slot, thr) ((void)0)
 #define TT_STAMP(kid, slot) ((void)0)
 #endif
 
 __device__ __forceinline__ int64_t step_for_first_kernel(const StepArgs& a) {
   return a.state ? a.state->step_done + 1 : a.step_host;
 }
+// The load goes through an explicit global pointer: written as a select
+// between a.state->step_cur and the kernel argument a.step_host it became a
+// FLAT load (generic address of either), whose wait is vmcnt(0) -- every load
+// issued before it then had to land before anything that depends on the step
+__device__ __forceinline__ int64_t load_step(const tt_state* st, const int64_t* dummy_global) {
+  typedef __attribute__((address_space(1))) const int64_t gi64;
+  const int64_t* p = st ? &st->step_cur : dummy_global;
+  return *(gi64*)p;
+}
 __device__ __forceinline__ int64_t step_current(const StepArgs& a) {
-  return a.state ? a.state->step_cur : a.step_host;
+  const int64_t v = load_step(a.state, reinterpret_cast<const int64_t*>(a.lsr));
+  return a.state ? v : a.step_host;
 }
 __device__ __forceinline__ int64_t batch_row0(const StepArgs& a, int64_t t) {
   if (a.cycle > 0) return ((t - 1 - a.t_base) % a.cycle) * a.B;

@@ -34,6 +34,8 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   __shared__ float xpart[4][RED_G][RED_E];  // kinds 3, 4: gg0, gbe0, sum Zh0, sum X' replicas
   TT_STAMP(5, 0);
   // the step first: a later load would make its wait (in-order vmcnt) wait for the slabs
+  // (a select of the two addresses: one FLAT load, issued first -- measured
+  // 0.2 us faster here than the global load the tower kernels use)
   const int64_t t = a.state ? a.state->step_cur : a.step_host;
   const int el = threadIdx.x & (RED_E - 1), pg = threadIdx.x / RED_E;
   const int64_t vb = (int64_t)blockIdx.x * RED_E;

@@ -1239,21 +1239,24 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
 // ---------------------------------------------------------------------------
 template <int R>
 struct FoldLds {
-  static constexpr int LDW = H0 + 4;       // W4 row-major [32][68]
-  static constexpr int LDT = R + 4;        // transposed images [col][row]
-  static constexpr int W4s = 0;
-  static constexpr int dZT = W4s + H1 * LDW;
-  static constexpr int A0T = dZT + H1 * LDT;
-  static constexpr int dead = A0T + H0 * LDT;   // end of the region dead after dW4 / dA0
-  // phase 3-4 (over the dead region and beyond): the bf16x3 images of dY0,
-  // Zh0 and X', channel / column major ([64][R] bf16 per plane, rows along
-  // the contraction), 16-B chunks XOR-swizzled by the row's low 4 bits
-  static constexpr int PL = H0 * R;              // one plane, bf16 units
+  // bf16x3 images (bf16 units, 3 planes each).  Phases 1-2: A0 channel-major
+  // [64][R] (fold_at, as the P | Q images), dZ4 row-major [R][32] and W4^T
+  // [64][32] (swz_dz), the operands of dW4 and dA0
+  static constexpr int PL = H0 * R;              // one [64][R] plane
+  static constexpr int PZ = R * H1;              // one dZ4 plane
+  static constexpr int PW4 = H0 * H1;            // one W4^T plane
+  static constexpr int A0i = 0;
+  static constexpr int dZi = A0i + 3 * PL;
+  static constexpr int W4i = dZi + 3 * PZ;
+  static constexpr int dead = W4i + 3 * PW4;     // end of the region dead after dW4 / dA0
+  // phase 3-4 (over the dead region and beyond): the images of dY0, Zh0 and
+  // X', channel / column major ([64][R] per plane, rows along the
+  // contraction), 16-B chunks XOR-swizzled by the row's low 4 bits
   static constexpr int img = 3 * PL;             // one image (3 planes)
   static constexpr int IY = 0, IZ = img, IX = 2 * img;
   static constexpr int imgs_f = 3 * img / 2;     // floats
-  static_assert(imgs_f >= dead, "images cover the dead region");
-  static_assert(IX / 2 >= dead, "X' image clear of the phase-2 operands (written during phase 2)");
+  static_assert(IX >= dead, "X' image clear of the phase-2 operands (written during phase 2)");
+  static_assert(dZi % 8 == 0 && W4i % 8 == 0, "16-B aligned images");
   static constexpr int db4 = imgs_f;             // [32]
   static constexpr int c1 = db4 + H1;            // k1 mb mg mean1 inv1 [5][32]
   static constexpr int c0 = c1 + 5 * H1;         // mean0 alpha0 beta0 inv0 [4][64]
@@ -1264,6 +1267,12 @@ struct FoldLds {
   static constexpr size_t bytes = sizeof(float) * (size_t)total;
   static_assert(R == 128, "16 chunks of 8 rows per image row: the swizzle covers a whole row");
 };
+
+// 8-B chunk swizzle of the 64-B-row images (dZ4 [R][32], W4^T [64][32]):
+// conflict-free 8-B stores of 4 rows x 4 chunks per 16 lanes, 16-B reads of
+// chunk pairs (the XOR is 0 or 4) and transposed reads of 8 rows x 4 chunks
+// per half wave
+__device__ __forceinline__ int swz_dz(int row) { return (((row >> 1) ^ (row >> 3)) & 1) << 2; }
 
 // bf16 offset of (row c, contraction index k) in a FoldLds image plane; the
 // chunk swizzle folds in c >> 4 so the X' writes (rows 4 xc + i for 16 lanes
@@ -1277,7 +1286,6 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   using L = FoldLds<R>;
   static_assert(R == 128, "8 waves: one dW4 tile and one P|Q strip per wave");
   constexpr int NTH = R * 4;
-  constexpr int LDW = L::LDW, LDT = L::LDT;
   constexpr int XK = R * (FOLD_MAX_KP / 4) / NTH;  // X' float4 per thread (4)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
@@ -1285,14 +1293,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   const int64_t step = step_current(a);
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  float* W4s = smem + L::W4s;
-  float* dZT = smem + L::dZT;
-  float* A0T = smem + L::A0T;
+  uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
   float* db4 = smem + L::db4;
   float* c1 = smem + L::c1;
   float* c0 = smem + L::c0;
   float* red = smem + L::red;
   TT_STAMP(3, 0);
+  TT_STAMP_T(4, 0, 448);
 
   // ---- phase 0: issue every load -- dY1, Z4, Z0 of this wave's rows (C
   // layout), W4, BN inputs, then (after the step load they depend on) the
@@ -1309,9 +1316,15 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) zz0[j][i] = T.Z0[row * H0 + 16 * j + r];
   }
-  static_assert(H1 * H0 / 4 == NTH, "W4: one float4 per thread");
-  const int we = (int)threadIdx.x;
-  const float4 w4v = *reinterpret_cast<const float4*>(T.W4 + (we >> 4) * H0 + 4 * (we & 15));
+  // W4^T image: wave w, lane l takes h0 = 16 (w & 3) + (l >> 2) and h1
+  // chunk 4 (w >> 2) + (l & 3): four W4 rows (4 scalar loads, lanes along h0)
+  static_assert(H1 * H0 / 4 == NTH, "W4: one chunk of 4 per thread");
+  const int w4r = 16 * (w & 3) + (l >> 2), w4c = 4 * (w >> 2) + (l & 3);
+  float4 w4v;
+  w4v.x = T.W4[(4 * w4c + 0) * H0 + w4r];
+  w4v.y = T.W4[(4 * w4c + 1) * H0 + w4r];
+  w4v.z = T.W4[(4 * w4c + 2) * H0 + w4r];
+  w4v.w = T.W4[(4 * w4c + 3) * H0 + w4r];
   const int c1i = min((int)threadIdx.x, H1 - 1), c0i = min(max((int)threadIdx.x - H1, 0), H0 - 1);
   const float f1inv = T.fin1[H1 + c1i], f1mean = T.fin1[c1i], g1v = T.g1[c1i];
   const float f0inv = T.fin0[H0 + c0i], f0mean = T.fin0[c0i], g0v = T.g0[c0i], be0v = T.be0[c0i];
@@ -1344,9 +1357,10 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   }
   if (threadIdx.x < H1) db4[threadIdx.x] = 0.f;
   if (threadIdx.x < 4 * H0) red[threadIdx.x] = 0.f;
-  *reinterpret_cast<float4*>(W4s + (we >> 4) * LDW + 4 * (we & 15)) = w4v;
+  put_planes4(hs + L::W4i + w4r * H1 + ((w4c ^ swz_dz(w4r)) * 4), L::PW4, w4v);
   __syncthreads();
   TT_STAMP(3, 1);
+  TT_STAMP_T(4, 1, 448);
 
   // ---- phase 1: X' gather issued (used in phase 3: its latency hides
   // behind this phase's arithmetic), dZ4, A0 / Zh0 recompute
@@ -1380,7 +1394,11 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
       const float v = c1[col] * (dy1[q][i] - c1[H1 + col] - zh * c1[2 * H1 + col]);
       dz[q][i] = row < a.B ? v : 0.f;
     }
-    store_tile_T(dZT, LDT, 16 * q, 16 * w, dz[q]);
+    {  // dZ4 image: quad transpose -> row 16w + 4g + (r & 3), columns 16q + (r & ~3) .. +3
+      const f32x4 tq = quad_transpose(dz[q]);
+      const int zr = 16 * w + 4 * g + (r & 3), zc = 4 * q + (r >> 2);
+      put_planes4(hs + L::dZi + zr * H1 + ((zc ^ swz_dz(zr)) * 4), L::PZ, make_float4(tq[0], tq[1], tq[2], tq[3]));
+    }
     const float cb = col_reduce(dz[q][0] + dz[q][1] + dz[q][2] + dz[q][3]);
     if (g == 0) atomicAdd(db4 + col, cb);
   }
@@ -1403,22 +1421,55 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
       a0[j][i] = ok ? av : 0.f;
       zh0[j][i] = ok ? (z - c0[col]) * c0[3 * H0 + col] : 0.f;
     }
-    store_tile_T(A0T, LDT, 16 * j, 16 * w, a0[j]);
+    put_planes4(hs + L::A0i + fold_at(col, 16 * w + 4 * g), L::PL, make_float4(a0[j][0], a0[j][1], a0[j][2], a0[j][3]));
   }
   __syncthreads();
   TT_STAMP(3, 2);
+  TT_STAMP_T(4, 2, 448);
 
   // ---- phase 2: dW4 = dZ4^T A0 (wave w: h1-tile w & 1, h0-tile w >> 1),
   // dA0 = dZ4 W4 on the wave's rows -> dY0, BN0-backward column partials
+  // (bf16x3: dZ4 read transposed as the A operand of dW4, K = the tile's rows)
   float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
   {
     const int p = w & 1, q = w >> 1;
-    f32x4 acc[1] = {zero4()};
-    strip_gemm_nt<1>(dZT + 16 * p * LDT, LDT, A0T + 16 * q * LDT, LDT, R, acc);
-    store_tile_rm_wt(slab, (int)T.so_W4 + 16 * p * H0 + 16 * q, H0, acc[0]);
+    const int qd = (l & 15) >> 2, pc = l & 3;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kk = 0; kk < R / 32; ++kk) {
+      const int ra = 32 * kk + 8 * g + qd, rb = ra + 4;
+      bf16x8 af[3], bf[3];
+#pragma unroll
+      for (int p3 = 0; p3 < 3; ++p3) {
+        const uint16_t* zb = hs + L::dZi + p3 * L::PZ;
+        af[p3] = tr_frag(zb + ra * H1 + (((4 * p + pc) ^ swz_dz(ra)) * 4), zb + rb * H1 + (((4 * p + pc) ^ swz_dz(rb)) * 4));
+        bf[p3] = *reinterpret_cast<const bf16x8*>(hs + L::A0i + p3 * L::PL + fold_at(16 * q + r, 32 * kk + 8 * g));
+      }
+      mfma_x3(af, bf, acc);
+    }
+    store_tile_rm_wt(slab, (int)T.so_W4 + 16 * p * H0 + 16 * q, H0, acc);
   }
-  f32x4 dA[4] = {zero4(), zero4(), zero4(), zero4()};
-  strip_gemm_tn<4>(dZT + 16 * w, LDT, W4s, LDW, H1, dA);
+  // dA0 = dZ4 W4 on the wave's rows (one 32-deep K step per h0 tile)
+  f32x4 dA[4];
+  {
+    bf16x8 af[3];
+    const int ar = 16 * w + r;
+#pragma unroll
+    for (int p3 = 0; p3 < 3; ++p3)
+      af[p3] = *reinterpret_cast<const bf16x8*>(hs + L::dZi + p3 * L::PZ + ar * H1 + (((2 * g) ^ swz_dz(ar)) * 4));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int wr = 16 * j + r;
+      bf16x8 bw[3];
+#pragma unroll
+      for (int p3 = 0; p3 < 3; ++p3)
+        bw[p3] = *reinterpret_cast<const bf16x8*>(hs + L::W4i + p3 * L::PW4 + wr * H1 + (((2 * g) ^ swz_dz(wr)) * 4));
+      dA[j] = zero4();
+      mfma_x3(af, bw, dA[j]);
+    }
+  }
+  TT_STAMP(3, 3);
+  TT_STAMP_T(4, 3, 448);
   const float scl = drop ? a.drop_scale : 1.f;
   float sg[4], sb[4], sz[4];
   f32x4 dyt[4];
@@ -1439,7 +1490,6 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   // X' image (clear of W4s|dZT|A0T) and its column sums while the GEMMs above drain
   const bool cok = xc < ((T.n_num + 3) >> 2);
   {
-    uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
     // X' = X - c on valid rows and columns, 0 elsewhere; column partial sums
     float d[XK][4];
 #pragma unroll
@@ -1467,17 +1517,19 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
       for (int i = 0; i < 4; ++i) atomicAdd(rs + i, sx[i]);
     }
   }
+  TT_STAMP(3, 4);
+  TT_STAMP_T(4, 4, 448);
   cols_to_lds<4>(sg, red);
   cols_to_lds<4>(sb, red + H0);
   cols_to_lds<4>(sz, red + 2 * H0);
   __syncthreads();  // every wave is past dW4 (A0T) and dA0 (W4s, dZT)
-  TT_STAMP(3, 3);
+  TT_STAMP(3, 5);
+  TT_STAMP_T(4, 5, 448);
 
   // ---- phase 3: bf16x3 images of dY0, Zh0 (from the accumulator layout:
   // channel 16j + r, rows 16w + 4g .. +3) over the dead f32 region (X'
   // went in during phase 2: columns 4xc .. +3 of rows xr0 .. +3)
   {
-    uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = 16 * j + r, o = fold_at(c, 16 * w + 4 * g);
@@ -1494,7 +1546,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
     }
   }
   __syncthreads();
-  TT_STAMP(3, 4);
+  TT_STAMP(3, 6);
+  TT_STAMP_T(4, 6, 448);
 
   // ---- phase 4: P | Q = [dY0 | Zh0]^T X' over the tile's rows (bf16x3,
   // K = rows in 32-row steps): wave w owns channels 16 (w & 3) .. +15 of P
@@ -1502,7 +1555,6 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
   // k_reduce_adam's lanes for 16 columns of P and the same 16 of Q read one
   // contiguous 128 B
   {
-    const uint16_t* hs = reinterpret_cast<const uint16_t*>(smem);
     const uint16_t* Ai = hs + (w < 4 ? L::IY : L::IZ);
     const uint16_t* Bi = hs + L::IX;
     const int kp = T.kp, KT = kp / 16;
@@ -1537,7 +1589,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
     atomicAdd(fr + 3 * H0 + threadIdx.x, red[3 * H0 + threadIdx.x]);  // sum X'
   }
   if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = db4[threadIdx.x];
-  TT_STAMP(3, 5);
+  TT_STAMP(3, 7);
+  TT_STAMP_T(4, 7, 448);
 }
 
 // ---------------------------------------------------------------------------

@@ -21,7 +21,9 @@ import torch  # noqa: E402
 
 from bench import CONFIGS  # noqa: E402
 
-NAMES = ["k_l0_fwd", "k_l4_fwd", "k_top", "k_bwd_mid", "k_bwd_first", "k_reduce_adam"]
+# kernel id 4: k_bwd_first on the six-kernel path; on the folded path (no
+# k_bwd_first) k_bwd_mid_fold stamps its wave 7 there (id 3 is its wave 0)
+NAMES = ["k_l0_fwd", "k_l4_fwd", "k_top", "k_bwd_mid", "k_bwd_first|mid_fold w7", "k_reduce_adam"]
 
 
 def main():

@@ -433,6 +433,25 @@ struct StepArgs {
 // Diagnostic phase stamps (separate -DTT_STAMPS build only; compiled out of
 // the product library).  s_memrealtime (100 MHz, chip-wide) per block/phase.
 // ---------------------------------------------------------------------------
+// Register budget per kernel as waves per SIMD (amdgpu_waves_per_eu upper
+// bound).  The dynamic LDS of the 8-wave kernels allows one block per CU (two
+// waves per SIMD), but without this the compiler sizes registers for the
+// occupancy __launch_bounds__ alone would allow (4 waves: 128 VGPRs) and
+// serialises the bf16x3 MFMA chains to fit.
+#define TT_WPE(n) __attribute__((amdgpu_waves_per_eu(1, n)))
+#ifndef TT_WPE_TOP
+#define TT_WPE_TOP 2
+#endif
+#ifndef TT_WPE_MID
+#define TT_WPE_MID 8
+#endif
+#ifndef TT_WPE_L0
+#define TT_WPE_L0 8
+#endif
+#ifndef TT_WPE_L4
+#define TT_WPE_L4 8
+#endif
+
 #ifdef TT_STAMPS
 extern __device__ uint64_t* g_tt_stamps;
 #define TT_STAMP_T(kid, slot, thr)                                                                      \

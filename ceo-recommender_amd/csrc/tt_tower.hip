@@ -321,7 +321,7 @@ __device__ __forceinline__ void zero_x8(const TowerDev& T, int c0, float (&x)[8]
 }
 
 template <int R, int KS, bool VEC>
-__global__ __launch_bounds__(R * 4) void k_l0_fwd(StepArgs a) {
+__global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) {
   constexpr int NTH = R * 4;
   constexpr int KC = 32 * KS, LDK = L0Lds<R>::ldk(KS), PL = H0 * LDK;
   constexpr int C4N = KC / 4, N4 = H0 * C4N, WPT = N4 / NTH;  // W0 float4 per thread
@@ -475,7 +475,7 @@ struct L4Lds {
 };
 
 template <int R>
-__global__ __launch_bounds__(R * 4) void k_l4_fwd(StepArgs a) {
+__global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) {
   constexpr int NTH = R * 4;
   constexpr int LD = L4Lds<R>::LD;
   constexpr int Z4PT = R * (H0 / 4) / NTH;  // float4 of Z0 per thread
@@ -677,7 +677,7 @@ __device__ __forceinline__ int swz_w(int d) { return ((d >> 2) & 1) << 2; }
 // normalisation) and stops; TOP_EMB_BWD takes dU / dV from the caller
 // instead of the cosine/MSE closed form.  Everything from dU on is shared.
 template <int NDT, int R, bool EMB>
-__global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
+__global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
   using L = TopLds<NDT, R>;
   constexpr int NTH = R * 4, NW = R / 16, DP = L::DP;
   constexpr int WF4 = DP * (H1 / 4);  // float4 of one tower's padded W8
@@ -848,14 +848,25 @@ __global__ __launch_bounds__(R * 4) void k_top(StepArgs a) {
     };
     bf16x8 fo[2][3], fs[2][3];
     if (!(EMB && bwd)) {  // the embedding backward needs no forward recompute
+#pragma unroll
+      for (int j = 0; j < NDT; ++j) {  // bias first: U = b + sum
+        accO[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + 16 * j + 4 * g);
+        accS[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + DP + 16 * j + 4 * g);
+      }
       ld(0, fo[0], fs[0]);
 #pragma unroll
       for (int j = 0; j < NDT; ++j) {
         if (j + 1 < NDT) ld(j + 1, fo[(j + 1) & 1], fs[(j + 1) & 1]);
-        accO[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + 16 * j + 4 * g);  // bias first: U = b + sum
-        accS[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + DP + 16 * j + 4 * g);
-        mfma_x3(fo[j & 1], po, accO[j]);
-        mfma_x3(fs[j & 1], ps, accS[j]);
+        // keep the next tile's reads above this tile's MFMAs (the scheduler
+        // otherwise sinks them next to their use, one LDS latency per step)
+        // and interleave the two independent accumulation chains
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          accO[j] = mfma_bf16(fo[j & 1][PA[q]], po[PB[q]], accO[j]);
+          accS[j] = mfma_bf16(fs[j & 1][PA[q]], ps[PB[q]], accS[j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -1282,7 +1293,7 @@ __device__ __forceinline__ int fold_at(int c, int k) {
 }
 
 template <int R, bool VEC>
-__global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
+__global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepArgs a) {
   using L = FoldLds<R>;
   static_assert(R == 128, "8 waves: one dW4 tile and one P|Q strip per wave");
   constexpr int NTH = R * 4;
@@ -1561,21 +1572,30 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid_fold(StepArgs a) {
     const int ca = 16 * (w & 3) + r;
     const int so = (int)T.so_W0 + 16 * (w & 3) * 2 * kp + (w < 4 ? 0 : 16);
     f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+    // all four column tiles every time (X' columns >= the input width are
+    // zero in the image; tiles j >= kp / 16 are not stored): a branch-free
+    // loop whose next K step's reads are pinned above this step's 24 MFMAs
+    // (four interleaved accumulation chains)
+    bf16x8 af[2][3], bf[2][4][3];
+    auto ldk = [&](int kk, bf16x8 (&a_)[3], bf16x8 (&b_)[4][3]) {
+      const int k0 = 32 * kk + 8 * g;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a_[p] = *reinterpret_cast<const bf16x8*>(Ai + p * L::PL + fold_at(ca, k0));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b_[j][p] = *reinterpret_cast<const bf16x8*>(Bi + p * L::PL + fold_at(16 * j + r, k0));
+      }
+    };
+    ldk(0, af[0], bf[0]);
 #pragma unroll
     for (int kk = 0; kk < R / 32; ++kk) {
-      const int k0 = 32 * kk + 8 * g;
-      bf16x8 af[3];
+      if (kk + 1 < R / 32) ldk(kk + 1, af[(kk + 1) & 1], bf[(kk + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) af[p] = *reinterpret_cast<const bf16x8*>(Ai + p * L::PL + fold_at(ca, k0));
+      for (int q = 0; q < 6; ++q)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j < KT) {
-          bf16x8 bf[3];
-#pragma unroll
-          for (int p = 0; p < 3; ++p) bf[p] = *reinterpret_cast<const bf16x8*>(Bi + p * L::PL + fold_at(16 * j + r, k0));
-          mfma_x3(af, bf, acc[j]);
-        }
-      }
+        for (int j = 0; j < 4; ++j) acc[j] = mfma_bf16(af[kk & 1][PA[q]], bf[kk & 1][j][PB[q]], acc[j]);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)

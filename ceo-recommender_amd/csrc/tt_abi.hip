@@ -319,7 +319,7 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.t_base = b->t_base;
   a.eps = d->bn_eps;
   a.momentum = d->bn_momentum;
-  const double thr = (double)d->dropout_p * 16777216.0;
+  const double thr = (double)d->dropout_p * 65536.0;  // 16-bit uniforms (tt_common.h dropout_keep_rk)
   a.drop_thr = (uint32_t)thr;
   a.drop_scale = a.drop_thr > 0 ? 1.0f / (1.0f - d->dropout_p) : 1.0f;
   a.D = d->latent;

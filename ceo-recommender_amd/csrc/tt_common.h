@@ -293,11 +293,15 @@ __host__ __device__ __forceinline__ uint64_t dropout_key(uint64_t seed, uint64_t
                (uint64_t)(tower * 2 + layer + 1) * 0x8CB92BA72F3D8DD7ull);
 }
 // Per element (row, column) of one stream: a 32-bit avalanche permutation
-// (lowbias32) keyed per row, h = P(rk ^ column * 0x9E3779B9) with
-// rk = P(row ^ key_lo) + key_hi; keep iff the top 24 bits of h >= p * 2^24.
-// A bijection of the column within a row; the row key is shared by a row's
-// elements (one permutation per element, not one 64-bit mix), which matters:
-// the masks are recomputed wherever the forward or backward needs them.
+// (lowbias32) keyed per row, rk = P(row ^ key_lo) + key_hi, and per PAIR of
+// columns h = P(rk ^ pid * 0x9E3779B9): the pair (c, c ^ 2^HB) shares h, the
+// element with bit HB clear takes its low 16 bits, the other the high 16;
+// keep iff that 16-bit uniform >= floor(p * 2^16).  HB follows how the
+// kernels hold a layer's columns, so both halves of a hash land in one lane:
+// layer 0 (A0, MFMA C layout: columns 16 apart) HB = 4, layer 1 (A1, k_top:
+// 8 consecutive columns per lane) HB = 0.  Two elements per permutation (two
+// quarter-rate multiplies each) halves the cost of recomputing the masks
+// wherever the forward or backward needs them.
 __host__ __device__ __forceinline__ uint32_t perm32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7FEB352Du;
@@ -309,12 +313,14 @@ __host__ __device__ __forceinline__ uint32_t perm32(uint32_t x) {
 __device__ __forceinline__ uint32_t dropout_row_key(uint64_t key, int64_t row) {
   return perm32((uint32_t)row ^ (uint32_t)key) + (uint32_t)(key >> 32);
 }
+template <int HB>
 __device__ __forceinline__ bool dropout_keep_rk(uint32_t rk, int col, uint32_t thr) {
-  return (perm32(rk ^ ((uint32_t)col * 0x9E3779B9u)) >> 8) >= thr;
+  const uint32_t c = (uint32_t)col;
+  const uint32_t pid = ((c >> (HB + 1)) << HB) | (c & ((1u << HB) - 1u));
+  const uint32_t h = perm32(rk ^ (pid * 0x9E3779B9u));
+  return (((c >> HB) & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
 }
-__device__ __forceinline__ bool dropout_keep(uint64_t key, int64_t row, int col, uint32_t thr) {
-  return dropout_keep_rk(dropout_row_key(key, row), col, thr);
-}
+constexpr int DROP_HB0 = 4, DROP_HB1 = 0;  // layer 0 (A0), layer 1 (A1)
 
 // ---------------------------------------------------------------------------
 // Kernel argument block (passed by value; lives in the kernarg segment).
@@ -409,7 +415,7 @@ struct StepArgs {
   tt_state* state;       // device counters (nullable: host mode)
   int64_t step_host;     // host-mode step number (dropout stream / Adam t)
   uint64_t seed;
-  uint32_t drop_thr;     // keep iff 24-bit hash >= drop_thr  (0: no dropout)
+  uint32_t drop_thr;     // keep iff 16-bit uniform >= drop_thr = floor(p 2^16)  (0: no dropout)
   float drop_scale;      // 1/(1-p) as fp32
   float eps, momentum;
   int train;

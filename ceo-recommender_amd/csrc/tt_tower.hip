@@ -80,7 +80,7 @@ __device__ __forceinline__ float bn_relu_drop(float z, float mean, float alpha, 
                                               uint32_t rk, int col, uint32_t thr, float scale) {
   float y = (z - mean) * alpha + beta;
   y = y > 0.f ? y : 0.f;
-  if (drop) y = dropout_keep_rk(rk, col, thr) ? y * scale : 0.f;
+  if (drop) y = dropout_keep_rk<DROP_HB0>(rk, col, thr) ? y * scale : 0.f;
   return y;
 }
 
@@ -497,6 +497,9 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   TT_STAMP(1, 0);
 
   // issue every load of the phase first (Z0 rows are padded: no clamp needed)
+  // (row-coalesced float4s: the two columns of a dropout hash pair sit in
+  // different lanes here, each lane evaluates its own -- measured cheaper
+  // than a pair-per-lane mapping's less coalesced Z0 reads)
   float4 z[Z4PT];
 #pragma unroll
   for (int k = 0; k < Z4PT; ++k) {
@@ -814,7 +817,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
         const uint64_t key = dropout_key(a.seed, (uint64_t)step, tau, 1);
         const uint32_t rk = dropout_row_key(key, row);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] = dropout_keep_rk(rk, 8 * g + e, a.drop_thr) ? y[e] * a.drop_scale : 0.f;
+        for (int e = 0; e < 8; ++e) y[e] = dropout_keep_rk<DROP_HB1>(rk, 8 * g + e, a.drop_thr) ? y[e] * a.drop_scale : 0.f;
       }
     };
     float a1o[8];

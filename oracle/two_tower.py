@@ -118,12 +118,18 @@ def dropout_keep_mask(seed: int, step: int, tower: int, layer: int,
     k_lo, k_hi = np.uint32(key & 0xFFFFFFFF), np.uint32(key >> 32)
     rows = (np.arange(n_rows, dtype=np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     cols = np.arange(width, dtype=np.uint32)
+    # columns c and c ^ 2^hb share one hash (pair id = c without bit hb): the
+    # low 16 bits for bit hb clear, the high 16 otherwise (tt_common.h
+    # dropout_keep_rk; hb = 4 for layer 0, 0 for layer 1)
+    hb = np.uint32(4 if layer == 0 else 0)
+    pid = ((cols >> (hb + np.uint32(1))) << hb) | (cols & ((np.uint32(1) << hb) - np.uint32(1)))
+    hi = ((cols >> hb) & np.uint32(1)).astype(bool)
     with np.errstate(over="ignore"):
         rk = _perm32(rows ^ k_lo) + k_hi                      # per-row key
-        h = _perm32(rk[:, None] ^ (cols[None, :] * np.uint32(0x9E3779B9)))
-    h = (h >> np.uint32(8)).astype(np.int64)  # 24 random bits
-    thr = int(p * 16777216.0)
-    return h >= thr
+        h = _perm32(rk[:, None] ^ (pid[None, :] * np.uint32(0x9E3779B9)))
+    u = np.where(hi[None, :], h >> np.uint32(16), h & np.uint32(0xFFFF)).astype(np.int64)  # 16 random bits
+    thr = int(p * 65536.0)
+    return u >= thr
 
 
 # --------------------------------------------------------------------------

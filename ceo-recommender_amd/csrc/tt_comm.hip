@@ -84,6 +84,10 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  // Adam's bias corrections (double pow, a long dependent chain) while the
+  // peers' flags are in flight, not after the wait
+  AdamCoef c{};
+  if (a.p) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
   // 3. wait for every rank's slice b (bounded)
   if (threadIdx.x < a.world) {
     const uint64_t* f = a.flags[a.rank] + (int64_t)threadIdx.x * a.blocks + b;
@@ -101,8 +105,6 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
   if (ok_s == 0) return;  // this slice keeps its parameters (err reports it)
   // 4. mean over ranks in rank order + Adam
   const float inv_w = 1.0f / (float)a.world;
-  AdamCoef c;
-  if (a.p) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
   for (int64_t e = lo + threadIdx.x; e < hi; e += AR_THREADS) {
     float s = 0.f;
     for (int q = 0; q < a.world; ++q)

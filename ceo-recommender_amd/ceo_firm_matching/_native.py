@@ -177,9 +177,10 @@ def make_desc(n_num: Sequence[int], cat_counts: Sequence[Sequence[int]],
 
 def step_plan(desc: TTModelDesc, batch: int) -> dict:
     """How one fused training step runs at this batch size (tt_step_plan)."""
-    info = (ctypes.c_int32 * 4)()
-    check(lib().tt_step_plan(ctypes.byref(desc), int(batch), info, 4), "tt_step_plan")
-    return {"folded_bn0_backward": bool(info[0]), "top_rows": info[1], "mid_rows": info[2], "kernels": info[3]}
+    info = (ctypes.c_int32 * 5)()
+    check(lib().tt_step_plan(ctypes.byref(desc), int(batch), info, 5), "tt_step_plan")
+    return {"folded_bn0_backward": bool(info[0]), "top_rows": info[1], "mid_rows": info[2], "kernels": info[3],
+            "top_pair": bool(info[4])}
 
 
 def param_count(desc: TTModelDesc) -> int:

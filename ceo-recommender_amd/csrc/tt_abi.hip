@@ -173,6 +173,7 @@ static void set_lds_attrs() {
                         (const void*)k_top<4, 128, false>, (const void*)k_top<8, 128, false>,
                         (const void*)k_top<4, 64, true>,  (const void*)k_top<8, 64, true>,
                         (const void*)k_top<4, 128, true>, (const void*)k_top<8, 128, true>,
+                        (const void*)k_top_pair<4>, (const void*)k_top_pair<8>,
                         (const void*)k_bwd_mid<ROWS>, (const void*)k_bwd_mid_fold<FOLD_ROWS, true>,
                         (const void*)k_bwd_mid_fold<FOLD_ROWS, false>, (const void*)k_bwd_first<ROWS>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
@@ -180,7 +181,8 @@ static void set_lds_attrs() {
 }
 
 struct Plan {
-  size_t lds_l0, lds_l4, lds_top, lds_mid, lds_first;
+  size_t lds_l0, lds_l4, lds_top, lds_mid, lds_first, lds_pair;
+  bool top_pair;    // training steps run k_top_pair (both towers per 64-row block)
   int ndt;
   int top_rows;     // row tile of k_top (64, or 128 for large batches)
   int n_tiles;      // 64-row tiles
@@ -198,8 +200,12 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   // 128-row k_top tiles once the grid still covers every CU twice over
 #ifdef TT_TOP_ROWS
   P->top_rows = TT_TOP_ROWS;
+  P->top_pair = false;
 #else
-  P->top_rows = B >= 16384 ? 128 : 64;
+  // from B = 16384 (256 blocks of 64 rows) the training step's k_top runs
+  // k_top_pair; its other modes take k_top's 64-row tiles (same slab count)
+  P->top_pair = B >= 16384;
+  P->top_rows = 64;
 #endif
   // the 64-row kernels cover the padded rows, so every workspace row that any
   // kernel reads was written earlier in the same step
@@ -214,10 +220,11 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   const int tl = P->ndt == 4 ? (P->top_rows == 64 ? TopLds<4, 64>::total : TopLds<4, 128>::total)
                              : (P->top_rows == 64 ? TopLds<8, 64>::total : TopLds<8, 128>::total);
   P->lds_top = sizeof(float) * (size_t)tl;
+  P->lds_pair = sizeof(float) * (size_t)(P->ndt == 4 ? PairLds<4>::total : PairLds<8>::total);
   P->lds_mid = P->fold ? FoldLds<FOLD_ROWS>::bytes : MidLds<ROWS>::bytes;
   P->lds_first = FirstLds<ROWS>::bytes(kpm);
   (void)emb;
-  for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first})
+  for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first, P->lds_pair})
     if (s > LDS_MAX) return TT_ERR_UNSUPPORTED;
   return TT_OK;
 }
@@ -488,7 +495,7 @@ static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev
   launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
 static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}) {
-  if (r.adam_slots)
+  if (r.adam_slots || !r.apply_adam)  // <true> reads no coefficients when there is no Adam
     launch(k_reduce_adam<true>, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
   else
     launch(k_reduce_adam<false>, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
@@ -507,6 +514,13 @@ static void launch_top_t(const StepArgs& a, const Plan& P, int grid_y, hipStream
     launch(k_top<8, 128, EMB>, grid, blk, P.lds_top, s, ev, a);
 }
 static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev = {}) {
+  if (a.mode == TOP_TRAIN && P.top_pair) {
+    if (P.ndt == 4)
+      launch(k_top_pair<4>, dim3(P.n_tiles_top), dim3(512), P.lds_pair, s, ev, a);
+    else
+      launch(k_top_pair<8>, dim3(P.n_tiles_top), dim3(512), P.lds_pair, s, ev, a);
+    return;
+  }
   if (a.mode == TOP_EMB_FWD || a.mode == TOP_EMB_BWD)
     launch_top_t<true>(a, P, grid_y, s, ev);
   else
@@ -547,6 +561,7 @@ int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32
   info[1] = P.top_rows;
   info[2] = P.fold ? FOLD_ROWS : ROWS;
   info[3] = P.fold ? 5 : 6;
+  if (n_info >= 5) info[4] = P.top_pair ? 1 : 0;
   return TT_OK;
 }
 

@@ -111,6 +111,17 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
       coef_done = true;
 #pragma unroll
       for (int k = 0; k < U2; ++k) acc += (pg + k * RED_G < n) ? x[k] : 0.f;
+    } else if (n <= RED_G * 2 * UNR) {
+      // up to 256 slabs (k_top_pair's 64-row W8 partials at B = 16384): both
+      // rounds of loads in flight at once (the loop below would wait for the
+      // first round before issuing the second)
+      float x[2 * UNR];
+#pragma unroll
+      for (int k = 0; k < 2 * UNR; ++k) x[k] = ldp(min(pg + k * RED_G, n - 1));
+      if (!PRE && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+      coef_done = true;
+#pragma unroll
+      for (int k = 0; k < 2 * UNR; ++k) acc += (pg + k * RED_G < n) ? x[k] : 0.f;
     } else {
       for (int p0 = pg; p0 < n; p0 += RED_G * UNR) {
         float x[UNR];

@@ -1069,6 +1069,358 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_top_pair : the training step's k_top at large batches with BOTH towers'
+// backward in one block of 64 rows: waves 0-3 take tower 0, waves 4-7 tower 1,
+// 16 rows each.  k_top's tile pair (one block per tower) computes both
+// towers' forward in both blocks; here each tower's forward is computed once
+// and U / V are exchanged through LDS (fp32, padded rows), which halves the
+// forward MFMAs and the BN1 / ReLU / dropout work per row.  Everything else
+// follows k_top (same fragment layouts, swizzles and closed-form dU); the
+// dW8 partials of a block cover 64 rows of both towers.
+// LDS: the W8 images of both towers (phases 0-3) are reused for tower 0's dU
+// image and the U / V exchange region for tower 1's, once dA1 has read W8.
+// ---------------------------------------------------------------------------
+template <int NDT>
+struct PairLds {
+  static constexpr int R = 64;
+  static constexpr int DP = 16 * NDT;
+  static constexpr int CH = DP / 4;      // 8-B chunks per dU image row
+  static constexpr int LDW = H1;         // W8 image row (bf16)
+  static constexpr int PW = DP * LDW;    // one W8 plane
+  static constexpr int PA1 = R * H1;     // one A1 plane
+  static constexpr int PU = R * DP;      // one dU plane
+  static constexpr int XLD = DP + 4;     // exchange row stride (floats): conflict-free float4 rows
+  // bf16 units
+  static constexpr int W8i = 0;                     // [tower][3][DP][LDW], phases 0-3
+  static constexpr int dU0 = 0;                     // tower 0's dU image [3][R][DP], after dA1
+  static constexpr int A1i = W8i + 2 * 3 * PW;      // [tower][3][R][H1]
+  static constexpr int XCi = A1i + 2 * 3 * PA1;     // exchange fp32 [tower][R][XLD], phases 2-3
+  static constexpr int dU1 = XCi;                   // tower 1's dU image, after dA1
+  static constexpr int xc_h = 2 * R * XLD * 2;      // exchange size, bf16 units
+  static constexpr int hend = XCi + (xc_h > 3 * PU ? xc_h : 3 * PU);
+  static_assert(2 * 3 * PW == 3 * PU, "tower 0's dU image replaces the two W8 images");
+  static_assert(A1i % 8 == 0 && XCi % 8 == 0 && hend % 8 == 0, "16-B aligned regions");
+  // fp32 region (float units)
+  static constexpr int b8s = hend / 2;              // [tower][DP] (0 for d >= D)
+  static constexpr int cf1 = b8s + 2 * DP;          // [tower][4][H1] mean | gamma*inv | beta | inv
+  static constexpr int red = cf1 + 8 * H1;          // [tower][2*H1] dgamma1 | dbeta1 partials
+  static constexpr int scal = red + 4 * H1;         // [0] loss part [1] dls part
+  static constexpr int rsc = scal + 4;              // [512] replica-sum scratch
+  static constexpr int rst = rsc + 512;             // [tower][2*H1] BN1 moment sums
+  static constexpr int total = rst + 4 * H1;
+};
+
+template <int NDT>
+__global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a) {
+  using L = PairLds<NDT>;
+  constexpr int R = L::R, NTH = 512, DP = L::DP;
+  constexpr int WF4 = DP * (H1 / 4);                // float4 of one tower's padded W8
+  constexpr int WPT = (2 * WF4 + NTH - 1) / NTH;    // both towers' W8: float4 per thread
+  static_assert(NDT % 2 == 0, "a dA1 K step pairs two latent tiles");
+  static_assert(2 * WF4 % NTH == 0, "whole W8 float4 rounds");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
+  const int64_t step = step_current(a);
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
+  const int tw = __builtin_amdgcn_readfirstlane(w >> 2);  // this wave's tower (uniform: scalar a.tw[tw] reads)
+  const int rl = 16 * (w & 3) + r;   // this lane's row in the tile
+  const int64_t row = r0 + rl;
+  const int D = a.D;
+  const TowerDev& T = a.tw[tw];
+  auto pick = [&](int t_, auto p0, auto p1) { return t_ ? p1 : p0; };
+  TT_STAMP(2, 0);
+
+  // ---- phase 0: every load -- own tower's Z4 slice, both W8 (raw), biases,
+  // logit_scale, (target, weight), BN1 inputs, BN1 moment replicas
+  float4 zs[2];
+  {
+    const float4* ps_ = reinterpret_cast<const float4*>(T.Z4 + row * H1 + 8 * g);
+    zs[0] = ps_[0];
+    zs[1] = ps_[1];
+  }
+  float4 wv[WPT];
+#pragma unroll
+  for (int k = 0; k < WPT; ++k) {
+    const int e = (int)threadIdx.x + k * NTH, tt = e / WF4;
+    const int el = min(e - tt * WF4, D * (H1 / 4) - 1);
+    wv[k] = reinterpret_cast<const float4*>(pick(tt, a.tw[0].W8, a.tw[1].W8))[el];
+  }
+  const int bt8 = (int)threadIdx.x / DP, bd8 = min((int)threadIdx.x % DP, D - 1);
+  const float b8v = threadIdx.x < 2 * DP ? pick(bt8 & 1, a.tw[0].b8, a.tw[1].b8)[bd8] : 0.f;
+  const float lsc = *a.logit_scale;
+  const float tg = a.tgw[2 * row], wt = a.tgw[2 * row + 1];
+  const int bt = ((int)threadIdx.x / H1) & 1, bc = (int)threadIdx.x % H1;
+  float bn_sh = 0.f, bn_rm = 0.f, bn_rv = 0.f, bn_g = 0.f, bn_be = 0.f;
+  if (w == 0) {
+    const bool have_rs = a.tw[0].rm1 != nullptr;
+    const float* g1p = pick(bt, a.tw[0].g1, a.tw[1].g1);
+    bn_sh = pick(bt, a.tw[0].shift1, a.tw[1].shift1)[bc];
+    bn_rm = (have_rs ? pick(bt, a.tw[0].rm1, a.tw[1].rm1) : g1p)[bc];
+    bn_rv = (have_rs ? pick(bt, a.tw[0].rv1, a.tw[1].rv1) : g1p)[bc];
+    bn_g = g1p[bc];
+    bn_be = pick(bt, a.tw[0].be1, a.tw[1].be1)[bc];
+  }
+  RepSum2<NTH, 2 * H1> rs;
+  rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
+  if (threadIdx.x < 2 * DP) smem[L::b8s + threadIdx.x] = (threadIdx.x % DP) < (unsigned)D ? b8v : 0.f;
+  if (threadIdx.x < 4 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;  // red + scal
+#pragma unroll
+  for (int k = 0; k < WPT; ++k) {
+    const int e = (int)threadIdx.x + k * NTH, tt = e / WF4, el = e - tt * WF4;
+    const int d = el >> 3, c = ((el & 7) ^ swz_w(d)) * 4;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    put_planes4(hs + L::W8i + tt * 3 * L::PW + d * L::LDW + c, L::PW, d < D ? wv[k] : z);
+  }
+  rs.finish(smem + L::rsc, smem + L::rst);
+  if (threadIdx.x < 2 * H1) {
+    float mean, inv;
+    bn_coefs_pre(a, H1, smem + L::rst + bt * 2 * H1, bn_sh, bn_rm, bn_rv, pick(bt, a.tw[0].rm1, a.tw[1].rm1),
+                 pick(bt, a.tw[0].rv1, a.tw[1].rv1), pick(bt, a.tw[0].nbt1, a.tw[1].nbt1),
+                 pick(bt, a.tw[0].fin1, a.tw[1].fin1), a.update_stats && blockIdx.x == 0, bc, &mean, &inv);
+    float* cf = smem + L::cf1 + bt * 4 * H1;
+    cf[bc] = mean;
+    cf[H1 + bc] = inv * bn_g;
+    cf[2 * H1 + bc] = bn_be;
+    cf[3 * H1 + bc] = inv;
+  }
+  __syncthreads();
+  TT_STAMP(2, 1);
+
+  // ---- phase 1: own tower's A1 slice (row rl, hidden 8g..8g+7): BN1 + ReLU
+  // + dropout of Z4, split into planes (the forward's B operand), A1 image
+  const bool drop = a.drop_thr > 0;
+  float a1s[8], z4s[8];
+  bf16x8 ps[3];
+  {
+    const f32x4* cf = reinterpret_cast<const f32x4*>(smem + L::cf1 + tw * 4 * H1 + 8 * g);
+    const f32x4 mu[2] = {cf[0], cf[1]}, al[2] = {cf[H1 / 4], cf[H1 / 4 + 1]}, be[2] = {cf[H1 / 2], cf[H1 / 2 + 1]};
+    const float zz[8] = {zs[0].x, zs[0].y, zs[0].z, zs[0].w, zs[1].x, zs[1].y, zs[1].z, zs[1].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      z4s[e] = zz[e];
+      const float v = (zz[e] - mu[e >> 2][e & 3]) * al[e >> 2][e & 3] + be[e >> 2][e & 3];
+      a1s[e] = v > 0.f ? v : 0.f;
+    }
+    if (drop) {
+      const uint64_t key = dropout_key(a.seed, (uint64_t)step, tw, 1);
+      const uint32_t rk = dropout_row_key(key, row);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        a1s[e] = dropout_keep_rk<DROP_HB1>(rk, 8 * g + e, a.drop_thr) ? a1s[e] * a.drop_scale : 0.f;
+    }
+    split8x3(a1s, ps);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      *reinterpret_cast<bf16x8*>(hs + L::A1i + (tw * 3 + p) * L::PA1 + rl * H1 + ((2 * g) ^ swz_a(rl)) * 4) = ps[p];
+  }
+  TT_STAMP(2, 2);
+
+  // ---- phase 2: own tower's forward, transposed (lane (r, g): U[row rl][16j
+  // + 4g + i]); tile pairs as two interleaved chains, the next pair's W8
+  // fragments read above the current pair's MFMAs
+  f32x4 accS[NDT];
+  {
+    const uint16_t* wb = hs + L::W8i + tw * 3 * L::PW;
+    auto ld = [&](int j, bf16x8 (&f)[3]) {
+      const int dr = 16 * j + r;
+      const int off = dr * L::LDW + ((2 * g) ^ swz_w(dr)) * 4;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(wb + p * L::PW + off);
+    };
+#pragma unroll
+    for (int j = 0; j < NDT; ++j) accS[j] = *reinterpret_cast<const f32x4*>(smem + L::b8s + tw * DP + 16 * j + 4 * g);
+    bf16x8 f[2][2][3];
+    ld(0, f[0][0]);
+    ld(1, f[0][1]);
+#pragma unroll
+    for (int jj = 0; jj < NDT / 2; ++jj) {
+      if (jj + 1 < NDT / 2) {
+        ld(2 * jj + 2, f[(jj + 1) & 1][0]);
+        ld(2 * jj + 3, f[(jj + 1) & 1][1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        accS[2 * jj] = mfma_bf16(f[jj & 1][0][PA[q]], ps[PB[q]], accS[2 * jj]);
+        accS[2 * jj + 1] = mfma_bf16(f[jj & 1][1][PA[q]], ps[PB[q]], accS[2 * jj + 1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // exchange: own U to LDS, the other tower's V back
+  float* xc = smem + L::XCi / 2;
+#pragma unroll
+  for (int j = 0; j < NDT; ++j)
+    *reinterpret_cast<f32x4*>(xc + (tw * R + rl) * L::XLD + 16 * j + 4 * g) = accS[j];
+  __syncthreads();  // exchange rows written; A1 images complete
+  f32x4 accO[NDT];
+#pragma unroll
+  for (int j = 0; j < NDT; ++j)
+    accO[j] = *reinterpret_cast<const f32x4*>(xc + ((1 - tw) * R + rl) * L::XLD + 16 * j + 4 * g);
+  TT_STAMP(2, 3);
+
+  // ---- phase 3: cosine (one row per lane), loss and dls (tower-0 waves),
+  // closed-form dU, dA1^T = W8^T dU
+  const bool valid = row < a.B;
+  const float s = expf(lsc);
+  float uv = 0.f, oo = 0.f, tt2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < NDT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uv += accS[j][i] * accO[j][i];
+      oo += accS[j][i] * accS[j][i];
+      tt2 += accO[j][i] * accO[j][i];
+    }
+  uv = col_reduce(uv);
+  oo = col_reduce(oo);
+  tt2 = col_reduce(tt2);
+  const float ino = __builtin_amdgcn_rsqf(oo);
+  const float int_ = __builtin_amdgcn_rsqf(tt2);
+  const float cs = uv * ino * int_;
+  const float sc = cs * s;
+  const float diff = sc - tg;
+  float ds = 2.f * diff * (wt * (1.f / (float)a.B));
+  const float loss_p = valid ? wt * diff * diff : 0.f;
+  ds = valid ? ds : 0.f;
+  if (tw == 0) {
+    if (a.score && g == 0 && valid) a.score[row] = sc;
+    const float lp = row_reduce16(loss_p), dp = row_reduce16(ds * sc);
+    if (l == 0) {
+      atomicAdd(smem + L::scal + 0, lp);
+      atomicAdd(smem + L::scal + 1, dp);
+    }
+  }
+  const float dc = ds * s;
+  const float ka = valid ? dc * ino * int_ : 0.f;
+  const float kb = valid ? dc * cs * ino * ino : 0.f;
+  const int qd = (l & 15) >> 2, pc = l & 3;
+  f32x4 dA[2] = {zero4(), zero4()};
+  bf16x8 du[NDT / 2][3];
+  {
+    const uint16_t* wb = hs + L::W8i + tw * 3 * L::PW;
+#pragma unroll
+    for (int t = 0; t < NDT / 2; ++t) {
+      float x[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[i] = ka * accO[2 * t][i] - kb * accS[2 * t][i];
+        x[4 + i] = ka * accO[2 * t + 1][i] - kb * accS[2 * t + 1][i];
+      }
+      split8x3(x, du[t]);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        bf16x8 wf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int d0 = 32 * t + 4 * g + qd, d1 = d0 + 16;
+          const uint16_t* b = wb + p * L::PW;
+          wf[p] = tr_frag(b + d0 * L::LDW + ((2 * pc + q) ^ swz_w(d0)) * 4, b + d1 * L::LDW + ((2 * pc + q) ^ swz_w(d1)) * 4);
+        }
+        mfma_x3(wf, du[t], dA[q]);
+      }
+    }
+  }
+  TT_STAMP(2, 4);
+
+  // ---- phase 4: dY1 = dA1 * mask * scale, dgamma1 / dbeta1 partials; the dU
+  // images once every wave is past the W8 reads and the exchange reads
+  const float* cf = smem + L::cf1 + tw * 4 * H1;
+  const float scl = drop ? a.drop_scale : 1.f;
+  float dy[8], sg[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int h = 8 * g + e;
+    dy[e] = a1s[e] > 0.f ? dA[e >> 2][e & 3] * scl : 0.f;
+    sg[e] = dy[e] * ((z4s[e] - cf[h]) * cf[3 * H1 + h]);
+  }
+  {
+    const uint32_t off = (uint32_t)((row * H1 + 8 * g) * 4);
+    st_wt16(T.dY1, off, f32x4{dy[0], dy[1], dy[2], dy[3]});
+    st_wt16(T.dY1, off + 16, f32x4{dy[4], dy[5], dy[6], dy[7]});
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float vg = row_reduce16(sg[e]), vb = row_reduce16(dy[e]);
+    if (r == 0) {
+      atomicAdd(smem + L::red + tw * 2 * H1 + 8 * g + e, vg);
+      atomicAdd(smem + L::red + tw * 2 * H1 + H1 + 8 * g + e, vb);
+    }
+  }
+  __syncthreads();  // W8 and exchange regions dead
+  {
+    const int su = swz_u<L::CH>(rl);
+    uint16_t* dUs = hs + (tw == 0 ? L::dU0 : L::dU1);
+#pragma unroll
+    for (int t = 0; t < NDT / 2; ++t)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const u32x4 v = __builtin_bit_cast(u32x4, du[t][p]);
+        uint16_t* base = dUs + p * L::PU + rl * DP;
+        *reinterpret_cast<u32x2*>(base + ((8 * t + g) ^ su) * 4) = (u32x2){v[0], v[1]};
+        *reinterpret_cast<u32x2*>(base + ((8 * t + 4 + g) ^ su) * 4) = (u32x2){v[2], v[3]};
+      }
+  }
+  __syncthreads();  // dU images, BN partials
+  TT_STAMP(2, 5);
+
+  // ---- phase 5: dW8 (as dW8^T[h][d]) and db8 of the wave's tower over the
+  // 64 rows (K = rows, two 32-row steps); its 4 waves own latent tiles
+  // (w & 3), (w & 3) + 4, ...
+  {
+    float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
+    const uint16_t* dUs = hs + (tw == 0 ? L::dU0 : L::dU1);
+    const uint16_t* a1b = hs + L::A1i + tw * 3 * L::PA1;
+    const bf16x8 ones = __builtin_bit_cast(bf16x8, (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+    for (int pt = w & 3; pt < NDT; pt += 4) {
+      f32x4 acc[2] = {zero4(), zero4()};
+      f32x4 accb = zero4();
+#pragma unroll
+      for (int kk = 0; kk < R / 32; ++kk) {
+        const int ra = 32 * kk + 8 * g + qd, rb = ra + 4;
+        bf16x8 bu[3], aa[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const uint16_t* u = dUs + p * L::PU;
+          bu[p] = tr_frag(u + ra * DP + ((4 * pt + pc) ^ swz_u<L::CH>(ra)) * 4,
+                          u + rb * DP + ((4 * pt + pc) ^ swz_u<L::CH>(rb)) * 4);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const uint16_t* v = a1b + p * L::PA1;
+            aa[q][p] = tr_frag(v + ra * H1 + ((4 * q + pc) ^ swz_a(ra)) * 4, v + rb * H1 + ((4 * q + pc) ^ swz_a(rb)) * 4);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) mfma_x3(aa[q], bu, acc[q]);
+#pragma unroll
+        for (int p = 2; p >= 0; --p) accb = mfma_bf16(ones, bu[p], accb);
+      }
+      const int d = 16 * pt + r;
+      if (d < D) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) st_wt16(slab, (uint32_t)((T.so_W8 + d * H1 + 16 * q + 4 * g) * 4), acc[q]);
+        if (g == 0) slab[T.so_b8 + d] = accb[0];
+      }
+    }
+  }
+  TT_STAMP(2, 6);
+
+  // ---- BN1 affine and logit_scale / loss partials into the replicas
+  if (threadIdx.x < 4 * H1) {
+    const int tt = (int)threadIdx.x / (2 * H1), k = (int)threadIdx.x % (2 * H1);
+    float* dst = k < H1 ? pick(tt, a.tw[0].gg1, a.tw[1].gg1) : pick(tt, a.tw[0].gbe1, a.tw[1].gbe1);
+    atomicAdd(&dst[rep_of_block() * BNG + (k % H1)], smem[L::red + threadIdx.x]);
+  }
+  if (threadIdx.x == 0) {
+    float* lr = a.lsr + rep_of_block() * LSR;
+    atomicAdd(lr, smem[L::scal + 1]);
+    atomicAdd(lr + 1, smem[L::scal + 0] / (float)a.B);
+  }
+  TT_STAMP(2, 7);
+}
+
+// ---------------------------------------------------------------------------
 // k_bwd_mid : BN1 backward -> dZ4 ; dW4, db4 ; dA0 = dZ4 W4 ; dY0 ; dgamma0/dbeta0
 // ---------------------------------------------------------------------------
 template <int R>
@@ -1837,6 +2189,8 @@ TT_L0(4)
 TT_L0(8)
 #undef TT_L0
 template __global__ void k_l4_fwd<64>(StepArgs);
+template __global__ void k_top_pair<4>(StepArgs);
+template __global__ void k_top_pair<8>(StepArgs);
 template __global__ void k_top<4, 64, false>(StepArgs);
 template __global__ void k_top<8, 64, false>(StepArgs);
 template __global__ void k_top<4, 128, false>(StepArgs);

@@ -1363,6 +1363,18 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
       }
   }
   __syncthreads();  // dU images, BN partials
+  // BN1 affine and logit_scale / loss partials into the replicas, issued here
+  // so their round trip overlaps dW8 instead of ending the kernel
+  if (threadIdx.x < 4 * H1) {
+    const int tt = (int)threadIdx.x / (2 * H1), k = (int)threadIdx.x % (2 * H1);
+    float* dst = k < H1 ? pick(tt, a.tw[0].gg1, a.tw[1].gg1) : pick(tt, a.tw[0].gbe1, a.tw[1].gbe1);
+    atomicAdd(&dst[rep_of_block() * BNG + (k % H1)], smem[L::red + threadIdx.x]);
+  }
+  if (threadIdx.x == 0) {
+    float* lr = a.lsr + rep_of_block() * LSR;
+    atomicAdd(lr, smem[L::scal + 1]);
+    atomicAdd(lr + 1, smem[L::scal + 0] / (float)a.B);
+  }
   TT_STAMP(2, 5);
 
   // ---- phase 5: dW8 (as dW8^T[h][d]) and db8 of the wave's tower over the
@@ -1406,17 +1418,6 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
   }
   TT_STAMP(2, 6);
 
-  // ---- BN1 affine and logit_scale / loss partials into the replicas
-  if (threadIdx.x < 4 * H1) {
-    const int tt = (int)threadIdx.x / (2 * H1), k = (int)threadIdx.x % (2 * H1);
-    float* dst = k < H1 ? pick(tt, a.tw[0].gg1, a.tw[1].gg1) : pick(tt, a.tw[0].gbe1, a.tw[1].gbe1);
-    atomicAdd(&dst[rep_of_block() * BNG + (k % H1)], smem[L::red + threadIdx.x]);
-  }
-  if (threadIdx.x == 0) {
-    float* lr = a.lsr + rep_of_block() * LSR;
-    atomicAdd(lr, smem[L::scal + 1]);
-    atomicAdd(lr + 1, smem[L::scal + 0] / (float)a.B);
-  }
   TT_STAMP(2, 7);
 }
 
@@ -1888,7 +1889,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
   cols_to_lds<4>(sg, red);
   cols_to_lds<4>(sb, red + H0);
   cols_to_lds<4>(sz, red + 2 * H0);
-  __syncthreads();  // every wave is past dW4 (A0T) and dA0 (W4s, dZT)
+  __syncthreads();  // every wave is past dW4 and dA0 (A0, dZ4, W4^T images)
   TT_STAMP(3, 5);
   TT_STAMP_T(4, 5, 448);
 

@@ -385,7 +385,9 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     }
     add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles_mid);
     add(s[TT_SLOT_G1], 2 * H1, 2, t, 0, 0, bng + 2 * H0, BNG);
-    add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], 0, t, L.so[t][4], P.n_tiles_top);
+    // k_top_pair's 64-row partials: more than one round of slab loads, split
+    const int k8 = P.n_tiles_top > RED_G * RED_UNR && P.n_tiles_top <= 2 * RED_G * RED_UNR ? 5 : 0;
+    add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], k8, t, L.so[t][4], P.n_tiles_top);
   }
   add(L.ls, 1, 2, 0, 0, 0, ws + W.lsr, LSR);
   // element space of k_reduce_adam: every range starts on a block (one
@@ -394,7 +396,8 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   int64_t vo = 0;
   for (int i = 0; i < k; ++i) {
     r.seg[i].voff = vo;
-    r.seg[i].vlen = r.seg[i].kind == 3 ? 2 * r.seg[i].len : r.seg[i].len;
+    const int64_t len = r.seg[i].len;
+    r.seg[i].vlen = r.seg[i].kind == 3 ? 2 * len : r.seg[i].kind == 5 ? (len + 31) / 32 * 64 : len;
     vo = round_up(vo + r.seg[i].vlen, RED_E);
   }
   r.vn = vo;

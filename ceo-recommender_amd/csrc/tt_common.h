@@ -676,6 +676,12 @@ constexpr int MAX_SEG = 48;
 #endif
 constexpr int RED_E = TT_RED_E;    // elements per k_reduce_adam block
 constexpr int RED_G = 512 / RED_E; // slab groups per element (512 threads, 16 slab loads in flight each)
+constexpr int RED_UNR = 16;        // slab loads in flight per lane
+// Seg kinds: 0 slab partials, 1 gacc, 2 replicas, 3 folded W0 (P | Q), 4
+// folded b0, 5 slab partials of 129..256 slabs split in two slab halves:
+// lanes el < 32 sum slabs [0, 128) of 32 elements, lanes el >= 32 the rest
+// of the same elements (k_top_pair's 64-row W8 partials: every block then
+// loads as much as a 128-slab block)
 
 struct Seg {
   int64_t off, len;      // range in the parameter arena

@@ -47,13 +47,17 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   const Seg& S = a.seg[si];
   const int kind = S.kind;
   const int64_t dv = vb + el - S.voff;
-  const bool live = dv < S.vlen;
+  // kind 5: element of this lane and its slab half
+  static_assert(RED_E == 64, "kind 5 pairs lanes el and el + 32");
+  const bool shalf = kind == 5 && (el & 32) != 0;
+  const int64_t ei5 = (dv >> 6) * 32 + (el & 31);
+  const bool live = kind == 5 ? ei5 < S.len : dv < S.vlen;
   // parameter element of this lane; kind 3: W0 element and which half (P / Q)
   const bool qhalf = kind == 3 && (el & 16) != 0;
   const int wi = kind == 3 ? (int)(dv >> 5) * 16 + (el & 15) : 0;
-  const int64_t e = S.off + (kind == 3 ? (int64_t)wi : dv);
+  const int64_t e = S.off + (kind == 3 ? (int64_t)wi : kind == 5 ? ei5 : dv);
   // the Adam state of this element is loaded up front: its latency overlaps the slab loads
-  const bool owner = pg == 0 && live && !qhalf;
+  const bool owner = pg == 0 && live && !qhalf && !shalf;
   const bool adam_here = owner && a.apply_adam;
   float pp = 0.f, pm = 0.f, pv = 0.f;
   if (adam_here) {
@@ -70,9 +74,9 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   AdamCoef c{};
   bool coef_done = PRE;
   int ch = 0, kx = 0;  // kinds 3, 4: W0 row / column of this element (kind 4: channel)
-  if (kind == 0 || kind == 3) {
-    constexpr int UNR = 16;  // slab loads in flight per lane
-    int64_t so = live ? dv : 0;
+  if (kind == 0 || kind == 3 || kind == 5) {
+    constexpr int UNR = RED_UNR;
+    int64_t so = live ? (kind == 5 ? ei5 : dv) : 0;
     if (kind == 3) {  // P[ch][kx] (or Q); group pg also takes replica pg of the fold sums
       ch = wi / S.in;
       kx = wi - ch * S.in;
@@ -100,7 +104,16 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
     const uint32_t o0 = (uint32_t)so * 4u, ldb = (uint32_t)a.slab_ld * 4u;
     auto ldp = [&](int p) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(o0 + (uint32_t)p * ldb), 0, 0)); };
     const int n = S.n_slabs;
-    if (n <= RED_G * (UNR / 2)) {
+    if (kind == 5) {  // this lane's slab half: [0, 128) or [128, n), one round of loads
+      const int pb = shalf ? RED_G * UNR : 0, ne = shalf ? n : min(n, RED_G * UNR);
+      float x[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) x[k] = ldp(min(pb + pg + k * RED_G, ne - 1));
+      if (!PRE && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+      coef_done = true;
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) acc += (pb + pg + k * RED_G < ne) ? x[k] : 0.f;
+    } else if (n <= RED_G * (UNR / 2)) {
       // few slabs for this block shape (e.g. 128-row tiles at B = 16384 with
       // 16 groups): half the loads, none of them a clamped repeat
       constexpr int U2 = UNR / 2;
@@ -111,17 +124,6 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
       coef_done = true;
 #pragma unroll
       for (int k = 0; k < U2; ++k) acc += (pg + k * RED_G < n) ? x[k] : 0.f;
-    } else if (n <= RED_G * 2 * UNR) {
-      // up to 256 slabs (k_top_pair's 64-row W8 partials at B = 16384): both
-      // rounds of loads in flight at once (the loop below would wait for the
-      // first round before issuing the second)
-      float x[2 * UNR];
-#pragma unroll
-      for (int k = 0; k < 2 * UNR; ++k) x[k] = ldp(min(pg + k * RED_G, n - 1));
-      if (!PRE && adam_here) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
-      coef_done = true;
-#pragma unroll
-      for (int k = 0; k < 2 * UNR; ++k) acc += (pg + k * RED_G < n) ? x[k] : 0.f;
     } else {
       for (int p0 = pg; p0 < n; p0 += RED_G * UNR) {
         float x[UNR];
@@ -186,7 +188,11 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   float gsum = 0.f;
 #pragma unroll
   for (int k = 0; k < RED_G; ++k) gsum += part[k][el];
-  if (kind >= 3) {
+  if (kind == 5) {  // then the second slab half of the same element (fixed order)
+#pragma unroll
+    for (int k = 0; k < RED_G; ++k) gsum += part[k][el + 32];
+  }
+  if (kind == 3 || kind == 4) {
     // dW0 = k0 (P - mb s - mg Q) + db0 c,  db0 = -k0 mg sum Zh0  (k_bwd_mid_fold)
     float gg = 0.f, zs = 0.f;
 #pragma unroll 4

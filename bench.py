@@ -349,7 +349,7 @@ def main():
     emit = _guard_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
@@ -413,9 +413,12 @@ def main():
         step_fn()
     torch.cuda.synchronize()
 
-    graph, chunk = None, 1
+    # chunks of 16 steps (measured: 10 -> 16 takes 0.8 us off a step, 20 /
+    # 25 / 40 add 0.3-1.1 us), the remainder of K in a second, shorter graph
+    graph, graph_rem, chunk = None, None, 1
     if use_graph:
-        chunk = max(c for c in range(1, 17) if args.steps % c == 0)
+        chunk = min(int(os.environ.get("CEO_BENCH_CHUNK_MAX", "16")), args.steps)
+        rem = args.steps % chunk
         ok = 1
         try:
             s = torch.cuda.Stream()
@@ -429,16 +432,23 @@ def main():
             with torch.cuda.graph(graph):  # recorded only: nothing executes during capture
                 for _ in range(chunk):
                     step_fn()
+            if rem:
+                graph_rem = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph_rem):
+                    for _ in range(rem):
+                        step_fn()
         except Exception as e:  # capture unsupported here: every rank falls back to eager steps
             print(f"bench: graph capture failed ({e!r}); eager steps", file=sys.stderr)
-            ok, graph = 0, None
+            ok, graph, graph_rem = 0, None, None
         if pg is not None:  # all ranks replay, or none does
             flag = torch.tensor([ok], device=dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if int(flag.item()) == 0:
-                graph = None
+                graph, graph_rem = None, None
         if graph is not None:
-            graph.replay()  # one more warm replay
+            graph.replay()  # one more warm replay (each graph)
+            if graph_rem is not None:
+                graph_rem.replay()
         torch.cuda.synchronize()
         if pg is not None:
             dist.barrier()
@@ -450,9 +460,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if graph is not None:
+    if graph is not None:  # exactly K steps: K // chunk full chunks + the remainder graph
         for _ in range(args.steps // chunk):
             graph.replay()
+        if graph_rem is not None:
+            graph_rem.replay()
     else:
         for _ in range(args.steps):
             step_fn()

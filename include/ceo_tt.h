@@ -112,7 +112,9 @@ int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out /* TT_NUM_OFFSETS 
  * towers, widths % 4 == 0 and <= 64: k_bwd_first is not launched),
  * info[1] = k_top row tile, info[2] = k_bwd_mid row tile, info[3] = kernels
  * per tt_train_step (5 or 6; the event slots of tt_train_step_ev are fixed:
- * l0, l4, top, mid, first, reduce -- slot 4 stays unrecorded when folded).
+ * l0, l4, top, mid, first, reduce -- slot 4 stays unrecorded when folded),
+ * info[4] (n_info >= 5) = 1 when the step's k_top is k_top_pair (both
+ * towers' backward per 64-row block; from B = 16384).
  * Replaces nothing in the reference (training.py:44-57 is one autograd
  * pass); a query for callers that time or trace the step.             */
 int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32_t n_info);

@@ -213,7 +213,9 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   P->n_tiles = (int)(padded_rows(B) / ROWS);
   P->n_tiles_top = (int)((P->n_tiles * ROWS) / P->top_rows);
   // folded only for batches that still give the 128-row kernel >= 64 tiles
-  // per tower: cfg 2 (B = 4096) measured 45.9 us folded vs 42.4 us not
+  // per tower: cfg 2 (B = 4096) measured 45.9 us folded vs 42.4 us not (r01);
+  // re-measured with this round's kernels: 44.1 vs 43.7 us (k_bwd_mid_fold
+  // takes 14.1 us on its 64 blocks: its per-block chain, not bandwidth)
   P->fold = L.fold_ok && B >= TT_FOLD_MIN_B;
   P->n_tiles_mid = P->fold ? (int)((P->n_tiles * ROWS) / FOLD_ROWS) : P->n_tiles;
   P->lds_l0 = L0Lds<ROWS>::bytes(kpm);

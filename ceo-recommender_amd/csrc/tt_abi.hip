@@ -389,7 +389,7 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles_mid);
     add(s[TT_SLOT_G1], 2 * H1, 2, t, 0, 0, bng + 2 * H0, BNG);
     // k_top_pair's 64-row partials: more than one round of slab loads, split
-    const int k8 = P.n_tiles_top > RED_G * RED_UNR && P.n_tiles_top <= 2 * RED_G * RED_UNR ? 5 : 0;
+    const int k8 = RED_E == 64 && P.n_tiles_top > RED_G * RED_UNR && P.n_tiles_top <= 2 * RED_G * RED_UNR ? 5 : 0;
     add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], k8, t, L.so[t][4], P.n_tiles_top);
   }
   add(L.ls, 1, 2, 0, 0, 0, ws + W.lsr, LSR);

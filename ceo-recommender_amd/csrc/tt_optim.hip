@@ -48,7 +48,7 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   const int kind = S.kind;
   const int64_t dv = vb + el - S.voff;
   // kind 5: element of this lane and its slab half
-  static_assert(RED_E == 64, "kind 5 pairs lanes el and el + 32");
+  static_assert(RED_E == 64 || RED_G * RED_UNR >= 256, "kind 5 (lanes el and el + 32) only at RED_E = 64");
   const bool shalf = kind == 5 && (el & 32) != 0;
   const int64_t ei5 = (dv >> 6) * 32 + (el & 31);
   const bool live = kind == 5 ? ei5 < S.len : dv < S.vlen;

@@ -53,10 +53,30 @@ PEAK_BF16X3_TFLOPS = round(2516.6 / 6, 1)
 KERNELS = ("k_l0_fwd", "k_l4_fwd", "k_top", "k_bwd_mid", "k_bwd_first", "k_reduce_adam")
 
 
+def flops_per_pair(nf, nc, D):
+    """Reference-algorithmic FLOPs of one training pair: the
+    Linear layers of both towers, forward + backward (dW for every layer, dX
+    for layers 4 and 8; dX of layer 0 is not needed without embeddings),
+    2 FLOPs per multiply-add.  cfg 3: 106,496; cfg 2: 65,536."""
+    per = lambda n_in: 2 * (2 * n_in * 64 + 3 * 64 * 32 + 3 * 32 * D)  # noqa: E731
+    return per(nf) + per(nc)
+
+
+def compulsory_bytes_per_pair(nf, nc, n_params, B):
+    """SURVEY 8d compulsory HBM bytes per pair: the pair's inputs (features,
+    target, weight) + the optimizer's 28 B/param/step spread over the batch.
+    cfg 3: 520 + 36 = 556 B."""
+    return 4 * (nf + nc + 2) + 28 * n_params / B
+
+
 def kernel_work(nf, nc, D, B, n_params, plan):
-    """Algorithmic FLOPs and HBM bytes per launch of each step kernel
-    (both towers; FLOPs count 2 per multiply-add; bytes = compulsory
-    activation / input / partial-slab traffic, fp32).  plan: tt_step_plan."""
+    """Reference-algorithmic FLOPs and HBM bytes per launch of each step
+    kernel (both towers; FLOPs count 2 per multiply-add; bytes = compulsory
+    activation / input / partial-slab traffic, fp32).  plan: tt_step_plan.
+    FLOPs are the reference's work, not the kernels': the folded BN0
+    backward's P = dY0^T X' and Q = Zh0^T X' products stand for
+    the reference's ONE dW0 = dZ0^T X, so k_bwd_mid_fold is charged dW4 +
+    dA0 + dW0 (cfg 3: 537 MFLOP), not the 805 MFLOP it issues."""
     f = 4
     kp = lambda n: -(-n // 16) * 16  # noqa: E731
     tiles = lambda rows: -(-B // rows)  # noqa: E731
@@ -67,8 +87,8 @@ def kernel_work(nf, nc, D, B, n_params, plan):
         "k_l4_fwd": 2 * 2 * B * 32 * 64,
         "k_top": 2 * (3 * B * D * 32) * 2,          # U,V fwd + dW8 + dA1, both towers
         "k_bwd_mid": 2 * 2 * (2 * B * 32 * 64)      # dW4 + dA0
-                     + (2 * 2 * B * 64 * (nf + nc) if fold else 0),  # P, Q (folded dW0)
-        "k_bwd_first": 0 if fold else 2 * B * 64 * (nf + nc),        # dW0
+                     + (2 * B * 64 * (nf + nc) if fold else 0),  # dW0 (folded: P, Q combine to it)
+        "k_bwd_first": 0 if fold else 2 * B * 64 * (nf + nc),    # dW0
         "k_reduce_adam": 0,
     }
     w0_slab = (2 * 64 * (kp(nf) + kp(nc))) if fold else (64 * (nf + nc) + 128)  # P | Q, or dW0 | db0
@@ -85,23 +105,54 @@ def kernel_work(nf, nc, D, B, n_params, plan):
     return fl, by
 
 
-def load_pmc_traffic(name):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary
-    (profiles/*pmc*.json written by tools/pmc_traffic.py), or None."""
+def _pmc_kernels():
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return {}
     try:
         with open(p) as fh:
-            d = json.load(fh)
-        return d.get("kernels", {}).get(name, {}).get("hbm_bytes_per_launch")
+            return json.load(fh).get("kernels", {})
     except Exception:
-        return None
+        return {}
+
+
+def load_pmc_traffic(name):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json written by tools/pmc_traffic.py), or None."""
+    return _pmc_kernels().get(name, {}).get("hbm_bytes_per_launch")
+
+
+def pmc_bytes_per_step(names):
+    """Sum of the PMC bytes per launch of the step's kernels (None if any is missing)."""
+    k = _pmc_kernels()
+    vals = [k.get(n, {}).get("hbm_bytes_per_launch") for n in names]
+    return None if not vals or any(v is None for v in vals) else float(sum(vals))
+
+
+def usable_cores():
+    """CPUs this process may actually run on: the cgroup CPU quota when one
+    is set (the GPU box gives each GPU a 16-CPU share of a 256-CPU host),
+    else the affinity mask.  os.cpu_count() counts the whole host."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except Exception:
+        pass
+    return (min(n, quota) if quota else n), n, quota
 
 
 def cpu_baseline(nf, nc, D, B):
     """Time the CPU oracle on a bounded sample of the same workload."""
     from oracle import two_tower as O
+    usable, affinity, quota = usable_cores()
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = usable if quota else (env_threads or usable)
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     n = 524_288
     g = torch.Generator().manual_seed(42)
     data = {
@@ -130,11 +181,16 @@ def cpu_baseline(nf, nc, D, B):
             cpu_model = next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
     except Exception:
         pass
-    return {"value": round(pairs / t_loop, 1), "unit": "pairs/s", "cores": torch.get_num_threads(),
+    torch.set_num_threads(prev_threads)
+    return {"value": round(pairs / t_loop, 1), "unit": "pairs/s", "cores": threads,
             "kind": "port",
             "sample": f"{n} pairs ({nf}x{nc} feats, D={D}, bs={B}, p=0.1), 1 epoch, oracle reference loop "
                       f"(per-sample Dataset + DataLoader(shuffle=True)) in {t_loop:.1f}s",
             "compute_only_pairs_per_s": round(pairs2 / t_comp, 1),
+            "cores_basis": ("cgroup CPU quota" if quota else
+                            ("OMP_NUM_THREADS: this GPU's CPU share on the pool's box" if env_threads
+                             else "sched affinity")),
+            "cgroup_quota_cpus": quota, "affinity_cpus": affinity,
             "os_cpu_count": os.cpu_count(), "cpu_model": cpu_model}
 
 
@@ -527,16 +583,21 @@ def main():
                 continue  # not launched: its work runs inside k_bwd_mid (folded BN0 backward)
             per[name] = sum(evs[k][2 * i].elapsed_time(evs[k][2 * i + 1]) for k in range(args.steps)) / args.steps * 1e3
         fl, by = kernel_work(nf, nc, D, B, a.params.numel(), plan)
-        if plan["folded_bn0_backward"]:  # report the kernel that ran under its own name
-            for d_ in (per, fl, by):
-                d_["k_bwd_mid_fold"] = d_.pop("k_bwd_mid")
+        for on, (old, new) in ((plan["folded_bn0_backward"], ("k_bwd_mid", "k_bwd_mid_fold")),
+                               (plan["top_pair"], ("k_top", "k_top_pair"))):
+            if on:  # report the kernel that ran under its own name
+                for d_ in (per, fl, by):
+                    d_[new] = d_.pop(old)
         dom = max(per, key=per.get)
         t_s = per[dom] * 1e-6
         tf = fl[dom] / t_s / 1e12
         gbs = by[dom] / t_s / 1e9
-        if tf / PEAK_FP32_TFLOPS >= gbs / PEAK_HBM_GBS:
+        # a kernel with GEMM work is priced on the MFMA roofline (its reference
+        # FLOPs), the gradient reduce on HBM; the other figure rides along
+        if fl[dom] > 0:
             roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(tf / PEAK_FP32_TFLOPS, 4), "algorithmic_per_launch": fl[dom]}
+                    "frac": round(tf / PEAK_FP32_TFLOPS, 4), "algorithmic_per_launch": fl[dom],
+                    "hbm_gbs_secondary": round(gbs, 1), "hbm_frac_secondary": round(gbs / PEAK_HBM_GBS, 4)}
         else:
             roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_per_launch": by[dom]}
@@ -544,6 +605,21 @@ def main():
         roof["avg_us"] = round(per[dom], 3)
         roof["traffic"] = load_pmc_traffic(dom)
         result["roofline"] = roof
+        # the whole step against the same peaks: reference FLOPs per pair x B
+        # over the timed ms_per_step, and the PMC bytes of all the step's
+        # kernels against SURVEY 8d's compulsory bytes per pair
+        fpp = flops_per_pair(nf, nc, D)
+        cbp = compulsory_bytes_per_pair(nf, nc, a.params.numel(), B)
+        step_s = elapsed / args.steps
+        pmc_step = pmc_bytes_per_step(list(per))
+        result["step_roofline"] = {
+            "flops_per_pair": fpp, "flops_per_step": fpp * B,
+            "achieved_tflops": round(fpp * B / step_s / 1e12, 2), "peak_tflops": PEAK_FP32_TFLOPS,
+            "frac_mfma": round(fpp * B / step_s / 1e12 / PEAK_FP32_TFLOPS, 4),
+            "compulsory_bytes_per_pair": round(cbp, 1), "compulsory_bytes_per_step": round(cbp * B),
+            "compulsory_gbs": round(cbp * B / step_s / 1e9, 1),
+            "pmc_bytes_per_step": pmc_step,
+            "pmc_over_compulsory": round(pmc_step / (cbp * B), 2) if pmc_step else None}
         result["kernel_us"] = {k: round(v, 3) for k, v in per.items()}
         result["step_plan"] = plan
         result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)

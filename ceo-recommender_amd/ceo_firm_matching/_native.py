@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 
 import torch
 
-TT_ABI_VERSION = 2
+TT_ABI_VERSION = 3
 TT_MAX_CAT = 16
 TT_SLOTS_PER_TOWER = 10
 TT_NUM_OFFSETS = 2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER + 1
@@ -29,7 +29,8 @@ _PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # CEO_TT_LIB: diagnostic override (e.g. the -DTT_STAMPS build); the in-tree library otherwise
 LIB_PATH = os.environ.get("CEO_TT_LIB") or os.path.join(_PKG_PARENT, "lib", "libceo_tt.so")
 EXPORTED = ("tt_abi_version", "tt_param_count", "tt_param_offsets", "tt_buffer_count",
-            "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_train_step", "tt_train_step_ev",
+            "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_backward_ex", "tt_embed_forward",
+            "tt_embed_backward", "tt_embed_backward_ex", "tt_train_step", "tt_train_step_ev",
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
             "tt_nce_workspace_bytes", "tt_nce_norms", "tt_nce_forward", "tt_nce_loss", "tt_nce_backward",
             "tt_rank_workspace_bytes", "tt_retrieval_ranks", "tt_step_plan",
@@ -101,6 +102,8 @@ def lib() -> ctypes.CDLL:
         "tt_backward": (I32, [D, P, Bt, P, U64, I64, P, I64, P, P]),
         "tt_embed_forward": (I32, [D, P, P, P, Bt, I32, U64, I64, P, I64, P, P]),
         "tt_embed_backward": (I32, [D, P, Bt, P, U64, I64, P, I64, P, P]),
+        "tt_backward_ex": (I32, [D, P, P, Bt, P, I32, U64, I64, P, I64, P, P, P, P]),
+        "tt_embed_backward_ex": (I32, [D, P, P, Bt, P, I32, U64, I64, P, I64, P, P, P, P]),
         "tt_train_step": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P]),
         "tt_train_step_ev": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P, ctypes.POINTER(P)]),
         "tt_adam_apply": (I32, [P, P, P, P, I64, H, P, I64, P]),
@@ -177,10 +180,10 @@ def make_desc(n_num: Sequence[int], cat_counts: Sequence[Sequence[int]],
 
 def step_plan(desc: TTModelDesc, batch: int) -> dict:
     """How one fused training step runs at this batch size (tt_step_plan)."""
-    info = (ctypes.c_int32 * 5)()
-    check(lib().tt_step_plan(ctypes.byref(desc), int(batch), info, 5), "tt_step_plan")
+    info = (ctypes.c_int32 * 6)()
+    check(lib().tt_step_plan(ctypes.byref(desc), int(batch), info, 6), "tt_step_plan")
     return {"folded_bn0_backward": bool(info[0]), "top_rows": info[1], "mid_rows": info[2], "kernels": info[3],
-            "top_pair": bool(info[4])}
+            "top_pair": bool(info[4]), "ndt": info[5]}
 
 
 def param_count(desc: TTModelDesc) -> int:

@@ -19,8 +19,8 @@ Drop-in for the reference ``ceo_firm_matching/model.py:14-89``:
 from __future__ import annotations
 
 import os
-
 import warnings
+import weakref
 from typing import Dict, Optional
 
 import numpy as np
@@ -235,23 +235,26 @@ class _FusedTwoTower(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dscore):
-        if not ctx.train:
-            raise NotImplementedError("backward through an eval-mode CEOFirmMatcher forward is not "
-                                      "supported by the fused kernels (call model.train())")
+        # train- or eval-mode backward (eval: BatchNorm as the affine map of the
+        # running statistics, no dropout -- what autograd of model.py:67-89
+        # gives after model.eval()), with the numeric inputs' gradients when
+        # they require grad (run_deep_extensions.py:564-590 integrated gradients)
         f_num, f_cat, c_num, c_cat = ctx.saved_tensors
         model = ctx.model
         arena = model._arena
         B = f_num.shape[0]
         grad = torch.empty_like(arena.params)
         ds = dscore.reshape(-1).to(torch.float32).contiguous()
+        dxf, dxc = _input_grad_buffers(ctx, f_num, c_num)
         batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
-        rc = N.lib().tt_backward(arena.desc, arena.params.data_ptr(), batch, ds.data_ptr(), ctx.seed,
-                                 ctx.step, ctx.ws.data_ptr(), ctx.ws_bytes, grad.data_ptr(),
-                                 N.stream_ptr(f_num.device))
-        N.check(rc, "tt_backward", B, 64)
+        rc = N.lib().tt_backward_ex(arena.desc, arena.params.data_ptr(), arena.buffers.data_ptr(), batch,
+                                    ds.data_ptr(), int(ctx.train), ctx.seed, ctx.step, ctx.ws.data_ptr(),
+                                    ctx.ws_bytes, grad.data_ptr(), N.ptr(dxf), N.ptr(dxc),
+                                    N.stream_ptr(f_num.device))
+        N.check(rc, "tt_backward_ex", B, 64)
         offs = N.param_offsets(arena.desc)
         grads = [grad[off:off + p.numel()].view_as(p) for _, p, off in model._named_slots(offs)]
-        return (None, None, None, None, None, *grads)
+        return (None, dxf, None, dxc, None, *grads)
 
 
 class _FusedTowerEmbeddings(torch.autograd.Function):
@@ -283,9 +286,6 @@ class _FusedTowerEmbeddings(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, du, dv):
-        if not ctx.train:
-            raise NotImplementedError("backward through eval-mode tower embeddings is not supported by the "
-                                      "fused kernels (call model.train())")
         f_num, f_cat, c_num, c_cat = ctx.saved_tensors
         model = ctx.model
         arena = model._arena
@@ -297,29 +297,62 @@ class _FusedTowerEmbeddings(torch.autograd.Function):
         if dv is not None:
             demb[1].copy_(dv)
         grad = torch.empty_like(arena.params)
+        dxf, dxc = _input_grad_buffers(ctx, f_num, c_num)
         batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
-        rc = N.lib().tt_embed_backward(arena.desc, arena.params.data_ptr(), batch, demb.data_ptr(), ctx.seed,
-                                       ctx.step, ctx.ws.data_ptr(), ctx.ws_bytes, grad.data_ptr(),
-                                       N.stream_ptr(f_num.device))
-        N.check(rc, "tt_embed_backward", B, 64)
+        rc = N.lib().tt_embed_backward_ex(arena.desc, arena.params.data_ptr(), arena.buffers.data_ptr(), batch,
+                                          demb.data_ptr(), int(ctx.train), ctx.seed, ctx.step, ctx.ws.data_ptr(),
+                                          ctx.ws_bytes, grad.data_ptr(), N.ptr(dxf), N.ptr(dxc),
+                                          N.stream_ptr(f_num.device))
+        N.check(rc, "tt_embed_backward_ex", B, 64)
         offs = N.param_offsets(arena.desc)
         grads = [grad[off:off + p.numel()].view_as(p) for _, p, off in model._named_slots(offs)]
-        return (None, None, None, None, None, *grads)
+        return (None, dxf, None, dxc, None, *grads)
 
 
+def _input_grad_buffers(ctx, f_num, c_num):
+    """dL/d(numeric input) outputs of the backward, for the inputs that
+    require grad (autograd marks them in ctx.needs_input_grad: forward's
+    arguments are (model, f_num, f_cat, c_num, c_cat, *params))."""
+    out = []
+    for i, x in ((1, f_num), (3, c_num)):
+        want = ctx.needs_input_grad[i] and x.dim() == 2 and x.shape[1] > 0
+        out.append(torch.empty(x.shape[0], x.shape[1], dtype=torch.float32, device=x.device) if want else None)
+    return out
+
+
+
+
+_CHECKED_CODES: Dict[tuple, "weakref.ref"] = {}
 
 
 def check_category_codes(cat: Optional[torch.Tensor], counts, what: str):
     """Raise IndexError when a categorical code is outside its embedding table,
     as the reference's nn.Embedding does (model.py:69,74); the fused kernels
-    would otherwise clamp it.  One reduction + host read per call, and only
-    for towers that have categorical columns."""
+    would otherwise clamp it.  Only towers with categorical columns pay
+    anything: a host tensor is checked on the host (no device sync); a device
+    tensor costs one reduction + host read the first time it is seen, then
+    never again while its storage and version counter are unchanged (batch-1
+    eval loops over one resident tensor do not sync per forward)."""
     if not counts or cat is None or cat.numel() == 0:
         return
     k = len(counts)
+    if cat.device.type == "cpu":
+        c = cat[:, :k].numpy()
+        if bool(((c < 0) | (c >= np.asarray(counts, dtype=np.int64)[None, :])).any()):
+            raise IndexError(f"{what}: category code out of range of its embedding table")
+        return
+    # the cache holds a weak reference to the checked tensor itself: a new
+    # tensor that reuses a freed one's storage never matches
+    key = (cat.data_ptr(), cat._version, tuple(cat.shape), tuple(cat.stride()), tuple(counts))
+    ref = _CHECKED_CODES.get(key)
+    if ref is not None and ref() is cat:
+        return
     hi = torch.tensor(counts, device=cat.device, dtype=cat.dtype)
     if bool(((cat[:, :k] < 0) | (cat[:, :k] >= hi)).any()):
         raise IndexError(f"{what}: category code out of range of its embedding table")
+    if len(_CHECKED_CODES) > 256:
+        _CHECKED_CODES.clear()
+    _CHECKED_CODES[key] = weakref.ref(cat)
 
 
 def _fused_inputs(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
@@ -327,11 +360,16 @@ def _fused_inputs(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
     if model.logit_scale.device != dev:
         raise RuntimeError(f"CEOFirmMatcher parameters are on {model.logit_scale.device}, inputs on {dev}")
     model.bind_arena()
+    g = model._geom
+    f_cat_in, c_cat_in = f_cat, c_cat
+    # host-side code check before the upload (no device sync)
+    for cat, counts, what in ((f_cat, g["cat_counts"][0], "firm_cat"), (c_cat, g["cat_counts"][1], "ceo_cat")):
+        if cat is not None and cat.device.type == "cpu" and cat.dim() == 2:
+            check_category_codes(cat.long(), counts, what)
     f_num = _as_f32(f_numeric, dev)
     c_num = _as_f32(c_numeric, dev)
     f_cat = _as_i64(f_cat, dev)
     c_cat = _as_i64(c_cat, dev)
-    g = model._geom
     for t, (num, cat) in enumerate(((f_num, f_cat), (c_num, c_cat))):
         if num.dim() != 2 or num.shape[1] != g["n_num"][t]:
             raise RuntimeError(f"tower {TOWERS[t]}: expected [B, {g['n_num'][t]}] numeric input, got {tuple(num.shape)}")
@@ -339,8 +377,10 @@ def _fused_inputs(model: CEOFirmMatcher, f_numeric, f_cat, c_numeric, c_cat):
             raise RuntimeError(f"tower {TOWERS[t]}: expected [B, {len(g['cat_counts'][t])}] categorical input")
     if f_num.shape[0] != c_num.shape[0]:
         raise RuntimeError("firm and CEO batches differ in size")
-    check_category_codes(f_cat, g["cat_counts"][0], "firm_cat")
-    check_category_codes(c_cat, g["cat_counts"][1], "ceo_cat")
+    for raw, cat, counts, what in ((f_cat_in, f_cat, g["cat_counts"][0], "firm_cat"),
+                                   (c_cat_in, c_cat, g["cat_counts"][1], "ceo_cat")):
+        if raw is None or raw.device.type != "cpu":  # host tensors were checked before the upload
+            check_category_codes(cat, counts, what)
     params = [p for _, p, _ in model._named_slots(N.param_offsets(model._arena.desc))]
     return f_num, f_cat, c_num, c_cat, params
 

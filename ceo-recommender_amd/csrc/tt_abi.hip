@@ -568,6 +568,7 @@ int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32
   info[2] = P.fold ? FOLD_ROWS : ROWS;
   info[3] = P.fold ? 5 : 6;
   if (n_info >= 5) info[4] = P.top_pair ? 1 : 0;
+  if (n_info >= 6) info[5] = P.ndt;
   return TT_OK;
 }
 
@@ -627,25 +628,47 @@ int32_t tt_embed_forward(const tt_model_desc* d, const float* params, float* buf
   return forward_impl(d, params, buffers, nbt, b, train, seed, step, ws, ws_bytes, nullptr, emb, stream);
 }
 
-static int32_t backward_impl(const tt_model_desc* d, const float* params, const tt_batch* b, const float* dscore,
-                             const float* demb, uint64_t seed, int64_t step, void* ws, int64_t ws_bytes,
-                             float* grad, tt_stream_t stream) {
+// The backward without the folded BN0 backward (k_bwd_mid + k_bwd_first):
+// eval-mode backward and input gradients need dZ0 per row, which the fold
+// never forms.
+static void unfold(Plan& P) {
+  P.fold = false;
+  P.n_tiles_mid = P.n_tiles;
+  P.lds_mid = MidLds<ROWS>::bytes;
+}
+
+static int32_t backward_impl(const tt_model_desc* d, const float* params, const float* buffers, const tt_batch* b,
+                             const float* dscore, const float* demb, int32_t train, uint64_t seed, int64_t step,
+                             void* ws, int64_t ws_bytes, float* grad, float* dx0, float* dx1, tt_stream_t stream) {
   if (!params || (!dscore && !demb) || !ws || !grad) return TT_ERR_ARG;
+  if (!train && !buffers) return TT_ERR_ARG;  // eval: running statistics
   Ctx c;
-  int rc = prepare(d, b, ws_bytes, 2, &c);
+  int rc = prepare(d, b, ws_bytes, train ? 2 : 0, &c);
   if (rc) return rc;
+  if ((dx0 && d->n_num[0] <= 0) || (dx1 && d->n_num[1] <= 0)) return TT_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+  if (b->n_rows == 0) {  // an empty eval batch: every gradient is zero
+    (void)hipMemsetAsync(grad, 0, sizeof(float) * c.L.n, s);
+    return launch_check();
+  }
+  if (!train || dx0 || dx1) unfold(c.P);
   float* w = (float*)ws;
-  // running-stat buffers are not touched by backward; pass a dummy-safe pointer
+  // running-stat buffers are read (eval) but never updated by a backward
   StepArgs a;
-  fill_args(a, d, c.L, c.W, c.P.fold, params, nullptr, nullptr, b, w);
-  a.train = 1;
+  fill_args(a, d, c.L, c.W, c.P.fold, params, train ? nullptr : const_cast<float*>(buffers), nullptr, b, w);
+  a.train = train ? 1 : 0;
   a.update_stats = 0;
   a.seed = seed;
   a.step_host = step;
   a.mode = demb ? TOP_EMB_BWD : TOP_BWD_GIVEN;
   a.dscore = dscore;
   a.demb = demb;
+  a.tw[0].dxn = dx0;
+  a.tw[1].dxn = dx1;
+  if (!train) {  // eval: no dropout, BN affine with the running statistics
+    a.drop_thr = 0;
+    a.drop_scale = 1.f;
+  }
   (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
   for (int t = 0; t < 2; ++t) (void)hipMemsetAsync(w + c.W.bng[t], 0, sizeof(float) * NREP * BNG, s);
   (void)hipMemsetAsync(w + c.W.lsr, 0, sizeof(float) * NREP * LSR, s);
@@ -662,13 +685,31 @@ static int32_t backward_impl(const tt_model_desc* d, const float* params, const 
 int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch* b, const float* dscore,
                     uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream) {
   if (!dscore) return TT_ERR_ARG;
-  return backward_impl(d, params, b, dscore, nullptr, seed, step, ws, ws_bytes, grad, stream);
+  return backward_impl(d, params, nullptr, b, dscore, nullptr, 1, seed, step, ws, ws_bytes, grad, nullptr, nullptr,
+                       stream);
+}
+
+int32_t tt_backward_ex(const tt_model_desc* d, const float* params, const float* buffers, const tt_batch* b,
+                       const float* dscore, int32_t train, uint64_t seed, int64_t step, void* ws, int64_t ws_bytes,
+                       float* grad, float* dx_firm, float* dx_ceo, tt_stream_t stream) {
+  if (!dscore) return TT_ERR_ARG;
+  return backward_impl(d, params, buffers, b, dscore, nullptr, train, seed, step, ws, ws_bytes, grad, dx_firm,
+                       dx_ceo, stream);
 }
 
 int32_t tt_embed_backward(const tt_model_desc* d, const float* params, const tt_batch* b, const float* demb,
                           uint64_t seed, int64_t step, void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream) {
   if (!demb) return TT_ERR_ARG;
-  return backward_impl(d, params, b, nullptr, demb, seed, step, ws, ws_bytes, grad, stream);
+  return backward_impl(d, params, nullptr, b, nullptr, demb, 1, seed, step, ws, ws_bytes, grad, nullptr, nullptr,
+                       stream);
+}
+
+int32_t tt_embed_backward_ex(const tt_model_desc* d, const float* params, const float* buffers, const tt_batch* b,
+                             const float* demb, int32_t train, uint64_t seed, int64_t step, void* ws,
+                             int64_t ws_bytes, float* grad, float* dx_firm, float* dx_ceo, tt_stream_t stream) {
+  if (!demb) return TT_ERR_ARG;
+  return backward_impl(d, params, buffers, b, nullptr, demb, train, seed, step, ws, ws_bytes, grad, dx_firm, dx_ceo,
+                       stream);
 }
 
 static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,

@@ -346,6 +346,7 @@ struct TowerDev {
   int64_t so_W0, so_b0, so_W4, so_b4, so_W8, so_b8;  // offsets inside one slab
   float* fr;                              // folded: [NREP][FRW] replicas (zeroed by k_l0_fwd)
   float *k0s, *xsh;                       // folded: inv0*gamma0 [64], shift row [64] (block 0 writes)
+  float* dxn;                             // backward: dL/d numeric input [B, n_num] (nullable; k_bwd_first)
 };
 
 enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2, TOP_EMB_FWD = 3, TOP_EMB_BWD = 4 };

@@ -65,6 +65,12 @@ __device__ __forceinline__ void bn_coefs_pre(const StepArgs& a, int H, const flo
   } else {
     mean = rm_c;
     var = rv_c;
+    // eval: publish the running-stat coefficients the eval-mode backward
+    // recomputes the activations with (block 0; every writer stores the same)
+    if (blockIdx.x == 0 && fin) {
+      fin[c] = mean;
+      fin[H + c] = 1.f / sqrtf(var + a.eps);
+    }
   }
   *mean_out = mean;
   *inv_out = 1.f / sqrtf(var + a.eps);
@@ -1483,8 +1489,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   if (threadIdx.x < H1) {
     const int c = threadIdx.x;
     c1[c] = f1inv * g1v;
-    c1[H1 + c] = rst[H1 + c] * invB;
-    c1[2 * H1 + c] = rst[c] * invB;
+    c1[H1 + c] = a.train ? rst[H1 + c] * invB : 0.f;  // eval: BN is affine, no batch-mean terms
+    c1[2 * H1 + c] = a.train ? rst[c] * invB : 0.f;
     c1[3 * H1 + c] = f1mean;
     c1[4 * H1 + c] = f1inv;
   } else if (threadIdx.x < H1 + H0) {
@@ -2032,8 +2038,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
     c0[c] = f0inv * g0v;
-    c0[H0 + c] = rst[H0 + c] * invB;
-    c0[2 * H0 + c] = rst[c] * invB;
+    c0[H0 + c] = a.train ? rst[H0 + c] * invB : 0.f;  // eval: BN is affine, no batch-mean terms
+    c0[2 * H0 + c] = a.train ? rst[c] * invB : 0.f;
     c0[3 * H0 + c] = f0mean;
     c0[4 * H0 + c] = f0inv;
     db0[c] = 0.f;
@@ -2153,18 +2159,29 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     strip_gemm_nt<1>(dZT + 16 * w * LDT, LDT, XT + 16 * kt * LDT, LDT, R, acc);
     put_w0(kt, acc[0]);
   }
-  if (emb) {
-    // dX = dZ0 W0 on the embedding columns -> scatter-add into the tables.
+  float* dxn = T.dxn;
+  if (emb || dxn) {
+    // dX = dZ0 W0: the embedding columns are scatter-added into the tables,
+    // the numeric columns (when the caller asked for input gradients,
+    // model.py:67 f_numeric / c_numeric.grad) stored row-major [B, n_num].
     // W0 (row-major [64][ldk]) takes over the X^T image's LDS.
     __syncthreads();
     float* W0s = XT;
     stage_w<NTH>(T.W0, H0, T.in_dim, kp, W0s, ldk);
     __syncthreads();
-    for (int ktt = T.n_num / 16; ktt < KT; ++ktt) {
+    for (int ktt = dxn ? 0 : T.n_num / 16; ktt < KT; ++ktt) {
       f32x4 dx[1] = {zero4()};
       strip_gemm_tn<1>(dZT + 16 * w, LDT, W0s + 16 * ktt, ldk, H0, dx);
       const int col = 16 * ktt + r;
-      if (col >= T.n_num && col < T.in_dim) {
+      if (col < T.n_num) {
+        if (dxn) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int64_t row = r0 + 16 * w + 4 * g + i;
+            if (row < a.B) dxn[row * T.n_num + col] = dx[0][i];
+          }
+        }
+      } else if (col < T.in_dim) {
         const int c = col - T.n_num;
         const int jj = c / T.emb_dim, e = c - jj * T.emb_dim;
 #pragma unroll

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TT_ABI_VERSION 2
+#define TT_ABI_VERSION 3
 #define TT_MAX_CAT 16      /* categorical columns per tower */
 
 /* status codes */
@@ -114,7 +114,9 @@ int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out /* TT_NUM_OFFSETS 
  * per tt_train_step (5 or 6; the event slots of tt_train_step_ev are fixed:
  * l0, l4, top, mid, first, reduce -- slot 4 stays unrecorded when folded),
  * info[4] (n_info >= 5) = 1 when the step's k_top is k_top_pair (both
- * towers' backward per 64-row block; from B = 16384).
+ * towers' backward per 64-row block; from B = 4096),
+ * info[5] (n_info >= 6) = latent tiles of 16 the top kernels are
+ * instantiated for (4: LATENT <= 64, 8: LATENT <= 128).
  * Replaces nothing in the reference (training.py:44-57 is one autograd
  * pass); a query for callers that time or trace the step.             */
 int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32_t n_info);
@@ -140,6 +142,21 @@ int32_t tt_backward(const tt_model_desc* d, const float* params, const tt_batch*
                     const float* dscore, uint64_t seed, int64_t step,
                     void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream);
 
+/* tt_backward for a forward of either mode, with optional input gradients
+ * (autograd of model.py:67-89 w.r.t. f_numeric / c_numeric as well as the
+ * parameters: run_deep_extensions.py:564-590 integrated gradients calls
+ * model.eval(), requires_grad_ on the numeric inputs and score.backward()).
+ *   train=1: as tt_backward (batch statistics, the forward's dropout stream);
+ *   train=0: the backward of an eval-mode tt_forward -- BatchNorm is the
+ *            affine map of the running statistics in `buffers` (no batch
+ *            coupling, B = 1 allowed), no dropout.
+ * dx_firm [B, n_num[0]], dx_ceo [B, n_num[1]]: dL/d(numeric input), row-major
+ * fp32 (nullable each).  grad[param_count] is overwritten.                   */
+int32_t tt_backward_ex(const tt_model_desc* d, const float* params, const float* buffers,
+                       const tt_batch* b, const float* dscore, int32_t train, uint64_t seed,
+                       int64_t step, void* ws, int64_t ws_bytes, float* grad,
+                       float* dx_firm, float* dx_ceo, tt_stream_t stream);
+
 /* Tower embeddings: the raw tower outputs U = firm_tower(x_f), V =
  * ceo_tower(x_c) before the L2 normalisation (contrastive.py:52-72
  * get_embeddings; model.py:69-77).  emb is [2][B][latent]: U rows then V
@@ -152,6 +169,11 @@ int32_t tt_embed_forward(const tt_model_desc* d, const float* params, float* buf
 int32_t tt_embed_backward(const tt_model_desc* d, const float* params, const tt_batch* b,
                           const float* demb, uint64_t seed, int64_t step,
                           void* ws, int64_t ws_bytes, float* grad, tt_stream_t stream);
+/* ... of either mode with optional input gradients (as tt_backward_ex) */
+int32_t tt_embed_backward_ex(const tt_model_desc* d, const float* params, const float* buffers,
+                             const tt_batch* b, const float* demb, int32_t train, uint64_t seed,
+                             int64_t step, void* ws, int64_t ws_bytes, float* grad,
+                             float* dx_firm, float* dx_ceo, tt_stream_t stream);
 
 /* One fused training step = training.py:44-57: forward, weighted MSE,
  * backward, and (apply_adam=1) the Adam update.  With apply_adam=0 only grad

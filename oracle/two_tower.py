@@ -158,7 +158,7 @@ def _bn_train(z, gamma, beta, rm, rv, momentum=BN_MOMENTUM, eps=BN_EPS):
 def _bn_eval(z, gamma, beta, rm, rv, eps=BN_EPS):
     invstd = 1.0 / torch.sqrt(rv + eps)
     zhat = (z - rm) * invstd
-    return zhat * gamma + beta
+    return zhat * gamma + beta, zhat, invstd
 
 
 def dropout_scale(p: float) -> float:
@@ -176,7 +176,7 @@ def forward(params: Dict[str, torch.Tensor], buffers: Dict[str, torch.Tensor],
     (p = 0 or eval).  ``cache`` holds what the closed-form backward needs.
     """
     dt = params["logit_scale"].dtype
-    cache = {"towers": []}
+    cache = {"towers": [], "train": bool(train)}
     newbuf = dict(buffers)
     outs = []
     for ti, t in enumerate(TOWERS):
@@ -198,8 +198,7 @@ def forward(params: Dict[str, torch.Tensor], buffers: Dict[str, torch.Tensor],
                 nbk = f"{t}_tower.{bn}.num_batches_tracked"
                 newbuf[nbk] = buffers[nbk] + 1
             else:
-                y = _bn_eval(z, g, be, buffers[rmk].to(dt), buffers[rvk].to(dt))
-                zhat, invstd = None, None
+                y, zhat, invstd = _bn_eval(z, g, be, buffers[rmk].to(dt), buffers[rvk].to(dt))
             r = torch.clamp(y, min=0)
             if train and masks is not None and (ti, li) in masks:
                 noise = masks[(ti, li)].to(dt) * dropout_scale(p)
@@ -240,18 +239,26 @@ def weighted_mse(score, target, weight):
     return loss, dscore
 
 
-def _bn_backward(dy, zhat, invstd, gamma):
+def _bn_backward(dy, zhat, invstd, gamma, train=True):
+    """native_batch_norm_backward: train mode through the batch statistics;
+    eval mode (running statistics) BatchNorm is an affine map per column."""
     n = dy.shape[0]
     dgamma = (dy * zhat).sum(0)
     dbeta = dy.sum(0)
     dzhat = dy * gamma
+    if not train:
+        return invstd * dzhat, dgamma, dbeta
     dz = invstd * (dzhat - dzhat.sum(0) / n - zhat * (dzhat * zhat).sum(0) / n)
     return dz, dgamma, dbeta
 
 
-def backward(params, cache, dscore) -> Dict[str, torch.Tensor]:
-    """Closed-form gradients of sum(dscore * score) w.r.t. every parameter."""
+def backward(params, cache, dscore, input_grads: bool = False) -> Dict[str, torch.Tensor]:
+    """Closed-form gradients of sum(dscore * score) w.r.t. every parameter
+    (autograd of model.py:67-89 in the mode the forward ran in).  With
+    input_grads, also "firm_numeric" / "ceo_numeric": the gradients w.r.t.
+    the numeric inputs (run_deep_extensions.py:564-590 reads f_num.grad)."""
     grads = {}
+    train = cache.get("train", True)
     s, cos, score = cache["s"], cache["cos"], cache["score"]
     grads["logit_scale"] = (dscore * score).sum()
     dc = (dscore * s)[:, None]
@@ -270,7 +277,7 @@ def backward(params, cache, dscore) -> Dict[str, torch.Tensor]:
             dr = da * noise if noise is not None else da
             dy = dr * (y > 0).to(dr.dtype)
             dz, dg, dbe = _bn_backward(dy, c[f"zhat{li}"], c[f"invstd{li}"],
-                                       params[f"{t}_tower.{bn}.weight"])
+                                       params[f"{t}_tower.{bn}.weight"], train)
             grads[f"{t}_tower.{bn}.weight"] = dg
             grads[f"{t}_tower.{bn}.bias"] = dbe
             h = c[f"h{li}"]
@@ -280,6 +287,9 @@ def backward(params, cache, dscore) -> Dict[str, torch.Tensor]:
         # da is now dX; scatter into the embedding tables (EmbeddingBackward)
         cat = c["cat"]
         n_emb = cat.shape[1]
+        if input_grads:
+            E_ = params[f"{t}_embeddings.0.weight"].shape[1] if n_emb else 0
+            grads[f"{t}_numeric"] = da[:, :c["x"].shape[1] - n_emb * E_]
         if n_emb:
             E = params[f"{t}_embeddings.0.weight"].shape[1]
             n_num = c["x"].shape[1] - n_emb * E

@@ -33,7 +33,11 @@ Fixtures:
   * ``contrastive_train.npz``: ``train_contrastive`` (contrastive.py:197-272),
       InfoNCE and triplet: one-step grads and a 2-epoch run (prints, final state).
 
-    python tests/golden/make_golden.py [contrastive|triplet|contrastive_train]   # only that fixture
+  * ``ig.npz``: eval-mode backward with input gradients -- the reference's
+      ``integrated_gradients`` (run_deep_extensions.py:550-603) and one
+      eval-mode weighted-MSE backward (parameter + numeric-input grads).
+
+    python tests/golden/make_golden.py [contrastive|triplet|contrastive_train|synthetic|ig]   # only that fixture
 """
 import contextlib
 import io
@@ -481,7 +485,65 @@ def gen_synthetic():
     np.savez_compressed(os.path.join(HERE, "synthetic.npz"), **out)
 
 
+def gen_ig():
+    """Eval-mode backward with input gradients (SURVEY 8a a12 in eval mode):
+    the reference's own integrated_gradients (run_deep_extensions.py:550-603:
+    model.eval(), requires_grad_ on the numeric inputs, score.backward(),
+    f_num.grad) on one input row, plus one eval-mode weighted-MSE backward of
+    a batch (parameter and input gradients), fp32 and fp64, for the
+    meta_test (embeddings) and cfg2 geometries."""
+    sys.path.insert(0, REF)
+    import run_deep_extensions as rde
+    out = {}
+    for name in ("meta_test", "cfg2"):
+        meta, latent, _ = CASES[name]
+        rng = np.random.default_rng(11)
+        cfg = make_config(latent)
+        torch.manual_seed(0)
+        model = CEOFirmMatcher(meta, cfg)
+        with torch.no_grad():
+            for tower in (model.firm_tower, model.ceo_tower):
+                for idx in (1, 5):
+                    bn = tower[idx]
+                    bn.running_mean.copy_(torch.from_numpy(rng.normal(0, 0.3, bn.running_mean.shape)
+                                                           .astype(np.float32)))
+                    bn.running_var.copy_(torch.from_numpy(rng.uniform(0.5, 2.0, bn.running_var.shape)
+                                                          .astype(np.float32)))
+        sd = {k: v.clone() for k, v in model.state_dict().items()}
+        put(out, f"{name}/state", sd)
+        out[f"{name}/latent"] = latent
+        bnp = make_batch(meta, 32, rng)
+        put(out, f"{name}/batch", bnp)
+        base = {"firm_numeric": np.zeros((1, meta["n_firm_numeric"]), np.float32),
+                "ceo_numeric": np.zeros((1, meta["n_ceo_numeric"]), np.float32)}
+        for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+            m = CEOFirmMatcher(meta, cfg).to(dt)
+            m.load_state_dict({k: (v.to(dt) if v.is_floating_point() else v) for k, v in sd.items()})
+            b = tt(bnp, dt)
+            m.eval()
+            f_num = b["firm_numeric"].clone().requires_grad_(True)
+            c_num = b["ceo_numeric"].clone().requires_grad_(True)
+            s = m(f_num, b["firm_cat"], c_num, b["ceo_cat"])
+            loss = (b["weights"] * (s - b["target"]) ** 2).mean()
+            loss.backward()
+            out[f"{name}/{tag}/score"] = s.detach().numpy()
+            out[f"{name}/{tag}/loss"] = loss.detach().numpy()
+            out[f"{name}/{tag}/dx_firm"] = f_num.grad.numpy()
+            out[f"{name}/{tag}/dx_ceo"] = c_num.grad.numpy()
+            put(out, f"{name}/{tag}/grad", {n: p.grad for n, p in m.named_parameters()})
+            inputs = {k: b[k][:1] for k in ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat")}
+            bl = {k: torch.from_numpy(v).to(dt) for k, v in base.items()}
+            ig = rde.integrated_gradients(m, inputs, bl, n_steps=8)
+            out[f"{name}/{tag}/ig_firm"] = np.asarray(ig["firm_numeric"])
+            out[f"{name}/{tag}/ig_ceo"] = np.asarray(ig["ceo_numeric"])
+    np.savez_compressed(os.path.join(HERE, "ig.npz"), **out)
+    print("wrote ig.npz")
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["ig"]:
+        gen_ig()
+        sys.exit(0)
     if sys.argv[1:] == ["synthetic"]:
         gen_synthetic()
         sys.exit(0)
@@ -502,3 +564,4 @@ if __name__ == "__main__":
     gen_triplet()
     gen_contrastive_train()
     gen_synthetic()
+    gen_ig()

@@ -147,3 +147,57 @@ def test_init_consumes_rng_like_reference():
     ref = sub(g, "init")
     for k in O.param_names(meta):
         assert normwise(P[k].numpy(), ref[k]) < 1e-6, k
+
+
+def _ig_case(case):
+    g = load_golden("ig")
+    meta = meta_of(load_golden(case))
+    sd = sub(g, f"{case}/state")
+    P = {k: torch.from_numpy(sd[k]).double() for k in O.param_names(meta)}
+    buf = {k: (torch.from_numpy(np.asarray(sd[k])) if "num_batches" in k else torch.from_numpy(sd[k]).double())
+           for k in O.buffer_names()}
+    batch = {k: torch.from_numpy(v) for k, v in sub(g, f"{case}/batch").items()}
+    return g, meta, P, buf, batch
+
+
+def oracle_integrated_gradients(P, buf, row, n_steps):
+    """The integrated-gradients path of run_deep_extensions.py:550-603 on the
+    oracle: eval-mode forward + backward at each of n_steps + 1 points from a
+    zero baseline to the row; mean input gradient x (input - baseline)."""
+    acc = {"firm_numeric": 0, "ceo_numeric": 0}
+    alphas = torch.linspace(0, 1, n_steps + 1)
+    for a in alphas:
+        b = dict(row)
+        for k in acc:
+            b[k] = (a.double() * row[k].double())
+        score, cache, _ = O.forward(P, buf, b, train=False)
+        grads = O.backward(P, cache, torch.ones_like(score), input_grads=True)
+        for k, t in (("firm_numeric", "firm"), ("ceo_numeric", "ceo")):
+            acc[k] = acc[k] + grads[f"{t}_numeric"]
+    return {k: (v / (n_steps + 1) * row[k].double()).reshape(-1).numpy() for k, v in acc.items()}
+
+
+@pytest.mark.parametrize("case", ["meta_test", "cfg2"])
+def test_eval_backward_and_input_grads(case):
+    """Eval-mode backward (running-stat BatchNorm, no dropout) with the
+    numeric inputs' gradients, vs the reference's autograd (fp64)."""
+    g, meta, P, buf, batch = _ig_case(case)
+    score, cache, _ = O.forward(P, buf, batch, train=False)
+    loss, dscore = O.weighted_mse(score, batch["target"], batch["weights"])
+    grads = O.backward(P, cache, dscore, input_grads=True)
+    assert normwise(score.numpy(), g[f"{case}/f64/score"].reshape(-1)) < 1e-12
+    assert abs(float(loss) - float(g[f"{case}/f64/loss"])) < 1e-12
+    ref = sub(g, f"{case}/f64/grad")
+    for n in O.param_names(meta):
+        assert normwise(grads[n].numpy(), ref[n]) < 1e-10, n
+    assert normwise(grads["firm_numeric"].numpy(), g[f"{case}/f64/dx_firm"]) < 1e-10
+    assert normwise(grads["ceo_numeric"].numpy(), g[f"{case}/f64/dx_ceo"]) < 1e-10
+
+
+@pytest.mark.parametrize("case", ["meta_test", "cfg2"])
+def test_integrated_gradients_vs_reference(case):
+    g, meta, P, buf, batch = _ig_case(case)
+    row = {k: v[:1] for k, v in batch.items()}
+    ig = oracle_integrated_gradients(P, buf, row, 8)
+    assert normwise(ig["firm_numeric"], g[f"{case}/f64/ig_firm"]) < 1e-10
+    assert normwise(ig["ceo_numeric"], g[f"{case}/f64/ig_ceo"]) < 1e-10

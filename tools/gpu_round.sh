@@ -8,7 +8,7 @@ TAG=${1:-dev}; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 180 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest_gpu rc=$rc"; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { rc=$?; echo "smoke failed rc=$rc"; tail $OUT/smoke.log; exit $rc; }
 tail -1 $OUT/smoke.log

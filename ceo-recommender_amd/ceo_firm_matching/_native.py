@@ -24,6 +24,7 @@ TT_ERR_ARG = -1
 TT_ERR_BATCH_TOO_SMALL = -2
 TT_ERR_UNSUPPORTED = -3
 TT_ERR_WORKSPACE = -4
+TT_FLAG_DETERMINISTIC = 1
 
 _PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # CEO_TT_LIB: diagnostic override (e.g. the -DTT_STAMPS build); the in-tree library otherwise
@@ -46,7 +47,7 @@ class TTModelDesc(ctypes.Structure):
                 ("emb_dim", ctypes.c_int32 * 2), ("latent", ctypes.c_int32),
                 ("cat_counts", (ctypes.c_int32 * TT_MAX_CAT) * 2),
                 ("dropout_p", ctypes.c_float), ("bn_eps", ctypes.c_float),
-                ("bn_momentum", ctypes.c_float)]
+                ("bn_momentum", ctypes.c_float), ("flags", ctypes.c_int32)]
 
 
 class TTBatch(ctypes.Structure):
@@ -161,7 +162,7 @@ def check(rc: int, what: str, batch: int = 0, width: int = 64):
 
 def make_desc(n_num: Sequence[int], cat_counts: Sequence[Sequence[int]],
               emb_dim: Sequence[int], latent: int, dropout_p: float = 0.1,
-              bn_eps: float = 1e-5, bn_momentum: float = 0.1) -> TTModelDesc:
+              bn_eps: float = 1e-5, bn_momentum: float = 0.1, flags: int = 0) -> TTModelDesc:
     d = TTModelDesc()
     for t in range(2):
         if len(cat_counts[t]) > TT_MAX_CAT:
@@ -175,7 +176,25 @@ def make_desc(n_num: Sequence[int], cat_counts: Sequence[Sequence[int]],
     d.dropout_p = float(dropout_p)
     d.bn_eps = float(bn_eps)
     d.bn_momentum = float(bn_momentum)
+    d.flags = int(flags)
     return d
+
+
+def deterministic_default() -> bool:
+    """Deterministic reductions when torch's deterministic-algorithms mode is
+    on (torch.use_deterministic_algorithms(True)) or CEO_TT_DETERMINISTIC=1."""
+    env = os.environ.get("CEO_TT_DETERMINISTIC")
+    if env is not None:
+        return env not in ("", "0")
+    return bool(torch.are_deterministic_algorithms_enabled())
+
+
+def set_deterministic(desc: TTModelDesc, on: bool) -> TTModelDesc:
+    if on:
+        desc.flags |= TT_FLAG_DETERMINISTIC
+    else:
+        desc.flags &= ~TT_FLAG_DETERMINISTIC
+    return desc
 
 
 def step_plan(desc: TTModelDesc, batch: int) -> dict:

@@ -27,12 +27,16 @@ DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "we
 
 class FusedTrainer:
     def __init__(self, model: CEOFirmMatcher, lr: float = 4e-4, betas=(0.9, 0.999), eps: float = 1e-8,
-                 max_batch: int = 256, seed: Optional[int] = None, process_group=None):
+                 max_batch: int = 256, seed: Optional[int] = None, process_group=None,
+                 deterministic: Optional[bool] = None):
         dev = model.logit_scale.device
         if dev.type != "cuda":
             raise RuntimeError("FusedTrainer needs the model on a HIP device")
         self.model = model
         self.device = dev
+        # bitwise-repeatable steps (TT_FLAG_DETERMINISTIC; None: the model's
+        # setting, which follows torch.use_deterministic_algorithms)
+        self.deterministic = deterministic
         self.arena = model.bind_arena()
         self.desc = self.arena.desc
         self.lib = N.lib()
@@ -94,8 +98,12 @@ class FusedTrainer:
                             n_rows=n_rows, cycle=cycle, t_base=t_base)
 
     # ------------------------------------------------------------------ steps
+    def is_deterministic(self) -> bool:
+        return self.model.is_deterministic() if self.deterministic is None else bool(self.deterministic)
+
     def _launch(self, batch, n_rows, apply_adam: bool):
         self.ensure_batch(n_rows)
+        N.set_deterministic(self.desc, self.is_deterministic())
         a = self.arena
         rc = self.lib.tt_train_step(self.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
                                     batch, self.hp, self.seed, self.state.data_ptr(), self.ws.data_ptr(),

@@ -67,6 +67,12 @@ class CEOFirmMatcher(nn.Module):
         self._arena: Optional[_Arena] = None
         self._stream_step = 0
         self._aten_warned = False
+        # deterministic reductions (TT_FLAG_DETERMINISTIC): None follows
+        # torch.use_deterministic_algorithms / CEO_TT_DETERMINISTIC
+        self.deterministic: Optional[bool] = None
+
+    def is_deterministic(self) -> bool:
+        return N.deterministic_default() if self.deterministic is None else bool(self.deterministic)
 
     @staticmethod
     def _tower(d_in: int, latent: int, p: float) -> nn.Sequential:
@@ -213,7 +219,7 @@ class _FusedTwoTower(torch.autograd.Function):
         L = N.lib()
         B = f_num.shape[0]
         train = bool(model.training)
-        desc = arena.desc
+        desc = N.set_deterministic(arena.desc, model.is_deterministic())
         ws_bytes = N.workspace_bytes(desc, max(B, 1))
         ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=f_num.device)
         if _POISON_WS:  # diagnostic: surface reads of workspace the kernels never wrote
@@ -227,6 +233,7 @@ class _FusedTwoTower(torch.autograd.Function):
         N.check(rc, "tt_forward", B, 64)
         ctx.model = model
         ctx.train = train
+        ctx.det = model.is_deterministic()
         ctx.seed, ctx.step = seed, step
         ctx.ws, ctx.ws_bytes = ws, ws_bytes
         ctx.n_params = len(params)
@@ -247,6 +254,7 @@ class _FusedTwoTower(torch.autograd.Function):
         ds = dscore.reshape(-1).to(torch.float32).contiguous()
         dxf, dxc = _input_grad_buffers(ctx, f_num, c_num)
         batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
+        N.set_deterministic(arena.desc, ctx.det)
         rc = N.lib().tt_backward_ex(arena.desc, arena.params.data_ptr(), arena.buffers.data_ptr(), batch,
                                     ds.data_ptr(), int(ctx.train), ctx.seed, ctx.step, ctx.ws.data_ptr(),
                                     ctx.ws_bytes, grad.data_ptr(), N.ptr(dxf), N.ptr(dxc),
@@ -268,6 +276,8 @@ class _FusedTowerEmbeddings(torch.autograd.Function):
         B = f_num.shape[0]
         D = arena.desc.latent
         train = bool(model.training)
+        ctx.det = model.is_deterministic()
+        N.set_deterministic(arena.desc, ctx.det)
         ws_bytes = N.workspace_bytes(arena.desc, max(B, 1))
         ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=f_num.device)
         if _POISON_WS:
@@ -299,6 +309,7 @@ class _FusedTowerEmbeddings(torch.autograd.Function):
         grad = torch.empty_like(arena.params)
         dxf, dxc = _input_grad_buffers(ctx, f_num, c_num)
         batch = N.make_batch(f_num, f_cat, c_num, c_cat, n_rows=B)
+        N.set_deterministic(arena.desc, ctx.det)
         rc = N.lib().tt_embed_backward_ex(arena.desc, arena.params.data_ptr(), arena.buffers.data_ptr(), batch,
                                           demb.data_ptr(), int(ctx.train), ctx.seed, ctx.step, ctx.ws.data_ptr(),
                                           ctx.ws_bytes, grad.data_ptr(), N.ptr(dxf), N.ptr(dxc),

@@ -31,7 +31,7 @@ constexpr size_t LDS_MAX = 160 * 1024;
 // layouts
 // ---------------------------------------------------------------------------
 struct Layout {
-  int in_dim[2], kp[2];
+  int in_dim[2], kp[2], n_num[2];
   int64_t emb_off[2][TT_MAX_CAT];
   int64_t slot[2][TT_SLOTS_PER_TOWER];
   int64_t ls;
@@ -73,6 +73,7 @@ static Layout make_layout(const tt_model_desc* d) {
   for (int t = 0; t < 2; ++t) {
     const int in = d->n_num[t] + d->n_cat[t] * d->emb_dim[t];
     L.in_dim[t] = in;
+    L.n_num[t] = d->n_num[t];
     L.kp[t] = (int)round_up(in, 16);
     L.fold_ok = L.fold_ok && d->n_cat[t] == 0 && in % 4 == 0 && L.kp[t] <= FOLD_MAX_KP;
   }
@@ -109,9 +110,13 @@ struct WsLayout {
   int64_t tgw;
   int64_t slab[2];
   int64_t gacc;
+  int64_t det[2], det_lsr;     // deterministic mode: per-block partial slots [n_tiles][DET_W] per tower, (dls, loss)
+  int64_t demb[2];             // deterministic mode: embedding-column dX per batch row [rows][emb_w] (-1: none)
   int64_t total;  // floats
   int n_tiles;
 };
+
+constexpr int DET_W = 256;     // widest cross-block accumulator of one block (FRW, 2 * H0 .. )
 
 // Per-row workspace arrays hold whole 128-row tiles (the kernels store rows
 // beyond B unconditionally into this padding instead of branching per row).
@@ -153,6 +158,12 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
   }
   W.tgw = take(rows * 2);
   for (int t = 0; t < 2; ++t) W.slab[t] = take((int64_t)W.n_tiles * L.slab_ld);
+  for (int t = 0; t < 2; ++t) W.det[t] = take((int64_t)W.n_tiles * DET_W);
+  W.det_lsr = take((int64_t)W.n_tiles * 2);
+  for (int t = 0; t < 2; ++t) {
+    const int ew = L.in_dim[t] - L.n_num[t];
+    W.demb[t] = ew > 0 ? take(rows * ew) : -1;
+  }
   W.total = off;
   return W;
 }
@@ -311,6 +322,9 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
     T.fr = ws + W.fr + (int64_t)t * NREP * FRW;
     T.k0s = ws + W.k0s[t];
     T.xsh = ws + W.xsh[t];
+    T.dslot = ws + W.det[t];
+    T.demb = W.demb[t] >= 0 ? ws + W.demb[t] : nullptr;
+    T.emb_w = L.in_dim[t] - L.n_num[t];
     if (fold) {  // the folded k_bwd_mid accumulates gg0 | gbe0 into the fold replicas
       T.gg0 = T.fr;
       T.gbe0 = T.fr + H0;
@@ -338,6 +352,8 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.logit_scale = params + L.ls;
   a.lsr = ws + W.lsr;
   a.tgw = ws + W.tgw;
+  a.det = (d->flags & TT_FLAG_DETERMINISTIC) ? 1 : 0;
+  a.dslot_lsr = ws + W.det_lsr;
 }
 
 // Segments of the parameter arena for k_reduce_adam: W/b ranges come from the
@@ -507,6 +523,51 @@ static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}) {
     launch(k_reduce_adam<false>, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
 }
 
+// Deterministic mode: fold the per-block partial slots the kernel of stage
+// `pt` just stored into replica 0 of each accumulator (k_det_fold), or
+// scatter the embedding gradients in batch-row order (k_det_scatter).
+enum DetPoint { DET_L0, DET_L4, DET_TOP, DET_MID, DET_FIRST };
+static void det_fold(const StepArgs& a, const Plan& P, DetPoint pt, hipStream_t s) {
+  if (!a.det) return;
+  if (pt == DET_FIRST) {
+    if (P.fold) return;
+    int tables = 0, maxq = 0;
+    for (int t = 0; t < 2; ++t)
+      for (int j = 0; j < a.tw[t].n_cat; ++j) {
+        ++tables;
+        maxq = std::max(maxq, a.tw[t].emb_rows[j] * a.tw[t].emb_dim);
+      }
+    if (tables)
+      hipLaunchKernelGGL(k_det_scatter, dim3((unsigned)((maxq + 255) / 256), (unsigned)tables), dim3(256), 0, s, a);
+    return;
+  }
+  DetFold f;
+  std::memset(&f, 0, sizeof(f));
+  int n = 0, wmax = 0;
+  auto add = [&](const float* src, float* dst, int slots, int width) {
+    f.src[n] = src;
+    f.dst[n] = dst;
+    f.n_slots[n] = slots;
+    f.width[n] = width;
+    wmax = std::max(wmax, width);
+    ++n;
+  };
+  for (int t = 0; t < 2; ++t) {
+    const TowerDev& T = a.tw[t];
+    if (pt == DET_L0) add(T.dslot, T.st0, P.n_tiles, 2 * H0);
+    if (pt == DET_L4) add(T.dslot, T.st1, P.n_tiles, 2 * H1);
+    if (pt == DET_TOP) add(T.dslot, T.gg1, P.n_tiles_top, 2 * H1);
+    if (pt == DET_MID) {
+      if (P.fold)
+        add(T.dslot, T.fr, P.n_tiles_mid, FRW);
+      else
+        add(T.dslot, T.gg0, P.n_tiles, 2 * H0);
+    }
+  }
+  if (pt == DET_TOP) add(a.dslot_lsr, a.lsr, P.n_tiles_top, 2);
+  hipLaunchKernelGGL(k_det_fold, dim3((unsigned)((wmax + 255) / 256), (unsigned)n), dim3(256), 0, s, f);
+}
+
 template <bool EMB>
 static void launch_top_t(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev) {
   const dim3 grid(P.n_tiles_top, grid_y), blk(4 * P.top_rows);
@@ -609,7 +670,9 @@ static int32_t forward_impl(const tt_model_desc* d, const float* params, float* 
     }
   }
   launch_l0(a, c.P, s);
+  if (train) det_fold(a, c.P, DET_L0, s);
   launch_l4(a, c.P, s);
+  if (train) det_fold(a, c.P, DET_L4, s);
   launch_top(a, c.P, 1, s);
   return launch_check();
 }
@@ -674,8 +737,11 @@ static int32_t backward_impl(const tt_model_desc* d, const float* params, const 
   (void)hipMemsetAsync(w + c.W.lsr, 0, sizeof(float) * NREP * LSR, s);
   if (c.P.fold) (void)hipMemsetAsync(w + c.W.fr, 0, sizeof(float) * 2 * NREP * FRW, s);
   launch_top(a, c.P, 2, s);
+  det_fold(a, c.P, DET_TOP, s);
   launch_mid(a, c.P, s);
+  det_fold(a, c.P, DET_MID, s);
   launch_first(a, c.P, s);
+  det_fold(a, c.P, DET_FIRST, s);
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   r.inv_b = 1.f / (float)b->n_rows;
   launch_reduce(r, s);
@@ -747,10 +813,15 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     return e;
   };
   launch_l0(a, c.P, s, ev(0));
+  det_fold(a, c.P, DET_L0, s);
   launch_l4(a, c.P, s, ev(1));
+  det_fold(a, c.P, DET_L4, s);
   launch_top(a, c.P, 2, s, ev(2));
+  det_fold(a, c.P, DET_TOP, s);
   launch_mid(a, c.P, s, ev(3));
+  det_fold(a, c.P, DET_MID, s);
   launch_first(a, c.P, s, ev(4));
+  det_fold(a, c.P, DET_FIRST, s);
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   r.inv_b = 1.f / (float)b->n_rows;
   for (int t = 0; t < 2; ++t) {

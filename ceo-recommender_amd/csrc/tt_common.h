@@ -347,6 +347,12 @@ struct TowerDev {
   float* fr;                              // folded: [NREP][FRW] replicas (zeroed by k_l0_fwd)
   float *k0s, *xsh;                       // folded: inv0*gamma0 [64], shift row [64] (block 0 writes)
   float* dxn;                             // backward: dL/d numeric input [B, n_num] (nullable; k_bwd_first)
+  // deterministic mode (StepArgs::det): cross-block partial sums go to
+  // per-block slots [blocks][width] (plain stores) instead of float atomics
+  // into replicas; k_det_fold sums the slots in block order into replica 0
+  float* dslot;
+  float* demb;                            // det: dX of the embedding columns [Bpad][emb_w] for k_det_scatter
+  int emb_w;                              // n_cat * emb_dim
 };
 
 enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2, TOP_EMB_FWD = 3, TOP_EMB_BWD = 4 };
@@ -434,7 +440,21 @@ struct StepArgs {
   int fr_zero_len;
   AdamSlot* adam_slots;  // non-null: k_l0_fwd makes sure slot t & 1 holds step t's coefficients
   float adam_lr, adam_b1, adam_b2, adam_eps;
+  int det;               // deterministic reductions (TT_FLAG_DETERMINISTIC): slots + k_det_fold
+  float* dslot_lsr;      // det: per-block (dls, loss) partials [blocks][2]
 };
+
+// A block's partial sum of cross-block accumulator c: a float atomic into
+// replica rep_of_block() (order of arrival decides the rounding), or in
+// deterministic mode a plain store into the block's own slot, which
+// k_det_fold then sums in block order (bitwise repeatable).
+__device__ __forceinline__ void xblock_add(bool det, float* rep, int rep_stride, float* slot, int width, int c,
+                                           float v) {
+  if (det)
+    slot[(int64_t)blockIdx.x * width + c] = v;
+  else
+    atomicAdd(&rep[rep_of_block() * rep_stride + c], v);
+}
 
 // ---------------------------------------------------------------------------
 // Diagnostic phase stamps (separate -DTT_STAMPS build only; compiled out of

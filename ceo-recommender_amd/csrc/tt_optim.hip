@@ -234,6 +234,75 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
 template __global__ void k_reduce_adam<true>(RedArgs);
 template __global__ void k_reduce_adam<false>(RedArgs);
 
+// ---------------------------------------------------------------------------
+// Deterministic mode (TT_FLAG_DETERMINISTIC).  The tower kernels store each
+// block's partial of a cross-block accumulator into its own slot instead of
+// a float atomic into a replica; k_det_fold sums the slots of every column in
+// a fixed order (8 interleaved partial sums over the slots, combined as a
+// fixed tree) into replica 0 -- the replicas the consumers then add are that
+// sum and zeros, so every step is bitwise repeatable.  Up to 4 arrays per
+// launch (blockIdx.y).
+// ---------------------------------------------------------------------------
+struct DetFold {
+  const float* src[4];
+  float* dst[4];
+  int n_slots[4], width[4];
+};
+
+__global__ __launch_bounds__(256) void k_det_fold(DetFold f) {
+  const int k = blockIdx.y;
+  const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int w = f.width[k], n = f.n_slots[k];
+  if (c >= w) return;
+  const float* s = f.src[k] + c;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int i = 0;
+#pragma unroll 4
+  for (; i + 8 <= n; i += 8)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += s[(int64_t)(i + q) * w];
+  for (; i < n; ++i) acc[i & 7] += s[(int64_t)i * w];
+  f.dst[k][c] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+// Embedding-table gradients in deterministic mode (model.py:69,74 backward,
+// EmbeddingBackward): block (x, y) owns 256 consecutive (code, element)
+// entries of categorical column y (towers' columns concatenated); it stages
+// the batch's codes in chunks and adds the rows' dX (k_bwd_first, T.demb) in
+// batch-row order.  Every entry of every table is written (codes absent from
+// the batch get 0), so the gacc arena needs no zeroing in between.
+constexpr int DET_SCAT_CHUNK = 2048;
+__global__ __launch_bounds__(256) void k_det_scatter(StepArgs a) {
+  __shared__ int codes[DET_SCAT_CHUNK];
+  int j = (int)blockIdx.y, t = 0;
+  if (j >= a.tw[0].n_cat) {
+    j -= a.tw[0].n_cat;
+    t = 1;
+  }
+  const TowerDev& T = a.tw[t];
+  const int E = T.emb_dim, rows = T.emb_rows[j];
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // entry code * E + e
+  if ((int64_t)blockIdx.x * blockDim.x >= (int64_t)rows * E) return;  // whole block past the table
+  const int code = (int)(q / E), e = (int)(q - (int64_t)code * E);
+  const bool live = code < rows;
+  const int64_t base = batch_row0(a, step_current(a));
+  const float* dx = T.demb + j * E + e;
+  float acc = 0.f;
+  for (int64_t r0 = 0; r0 < a.B; r0 += DET_SCAT_CHUNK) {
+    const int n = (int)min((int64_t)DET_SCAT_CHUNK, a.B - r0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      int64_t c = T.cat[data_row(a, base, r0 + i) * T.cat_ld + j];
+      codes[i] = (int)(c < 0 ? 0 : (c >= rows ? rows - 1 : c));  // the kernels' clamp
+    }
+    __syncthreads();
+    if (live)
+      for (int i = 0; i < n; ++i)
+        if (codes[i] == code) acc += dx[(r0 + i) * T.emb_w];
+  }
+  if (live) T.gemb[j][q] = acc;
+}
+
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ P, const float* __restrict__ G,
                                               float* __restrict__ M, float* __restrict__ V, int64_t n,
                                               float lr, float b1, float b2, float eps, tt_state* state,

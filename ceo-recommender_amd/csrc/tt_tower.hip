@@ -161,15 +161,25 @@ struct RepSum2 {
   }
 };
 
-// Block-wide column sums of NT C-layout tiles into LDS `red` (ds_add_f32).
+// Block-wide column sums of NT C-layout tiles: wave w stores its column
+// totals into its own LDS row red[w * ld + ...] (no LDS atomics, whose
+// arrival order would decide the rounding); wave_rows_sum adds the rows in
+// wave order, so a block's sum is bitwise repeatable.
 template <int NT>
-__device__ __forceinline__ void cols_to_lds(const float (&s)[NT], float* red) {
-  const int l = lane_id(), r = l & 15, g = l >> 4;
+__device__ __forceinline__ void cols_to_lds(const float (&s)[NT], float* red, int ld) {
+  const int l = lane_id(), r = l & 15, g = l >> 4, w = wave_id();
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const float v = col_reduce(s[j]);
-    if (g == 0) atomicAdd(&red[16 * j + r], v);
+    if (g == 0) red[w * ld + 16 * j + r] = v;
   }
+}
+template <int NW>
+__device__ __forceinline__ float wave_rows_sum(const float* red, int ld, int c) {
+  float v = red[c];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) v += red[w * ld + c];
+  return v;
 }
 
 // Dataset rows of this tile (clamped into the batch) -> LDS.
@@ -293,9 +303,9 @@ constexpr int l0_ks(int kp) { return kp <= 32 ? 1 : kp <= 64 ? 2 : kp <= 128 ? 4
 template <int R>
 struct L0Lds {
   __host__ __device__ static constexpr int ldk(int ks) { return 32 * ks + 16; }  // 32-B pad: conflict-free reads
-  // bf16 planes [3][H0][ldk] | red [2*H0] | shl [H0]
+  // bf16 planes [3][H0][ldk] | red [4 waves][2*H0] | shl [H0]
   static size_t bytes(int kp) {
-    return sizeof(uint16_t) * 3 * (size_t)H0 * ldk(l0_ks(kp)) + sizeof(float) * 3 * H0;
+    return sizeof(uint16_t) * 3 * (size_t)H0 * ldk(l0_ks(kp)) + sizeof(float) * 9 * H0;
   }
 };
 
@@ -341,8 +351,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
   const int in = T.in_dim;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   uint16_t* Wh = reinterpret_cast<uint16_t*>(smem);
-  float* red = reinterpret_cast<float*>(Wh + 3 * PL);  // [128]
-  float* shl = red + 2 * H0;                           // [64] moment shift = Z0 of batch row 0
+  float* red = reinterpret_cast<float*>(Wh + 3 * PL);  // [4 waves][128]
+  float* shl = red + 4 * 2 * H0;                       // [64] moment shift = Z0 of batch row 0
   TT_STAMP(0, 0);
 
   // ---- issue (straight line): row indices; W0 (raw, clamped); this lane's
@@ -371,7 +381,6 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = T.b0[16 * j + r];
   const float bsh = T.b0[16 * w + r];
-  if (threadIdx.x < 2 * H0) red[threadIdx.x] = 0.f;
   // W0 image: zero columns >= in, split, store
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
@@ -436,8 +445,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
     }
   }
   if (a.train) {
-    cols_to_lds<4>(s1, red);
-    cols_to_lds<4>(s2, red + H0);
+    cols_to_lds<4>(s1, red, 2 * H0);
+    cols_to_lds<4>(s2, red + H0, 2 * H0);
   }
   // Z0 (workspace rows are padded to whole tiles: no guard), row-major via
   // quad transposes, 16-B write-through stores
@@ -458,7 +467,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
   }
   if (a.train) {
     __syncthreads();
-    if (threadIdx.x < 2 * H0) atomicAdd(&T.st0[rep_of_block() * 2 * H0 + threadIdx.x], red[threadIdx.x]);
+    if (threadIdx.x < 2 * H0)
+      xblock_add(a.det, T.st0, 2 * H0, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<4>(red, 2 * H0, threadIdx.x));
   }
   // the folded BN0 backward's replicas start every step at zero (k_bwd_mid
   // accumulates them, k_reduce_adam only reads them)
@@ -477,7 +487,7 @@ template <int R>
 struct L4Lds {
   static constexpr int LD = H0 + 4;
   static constexpr size_t bytes =
-      sizeof(float) * ((size_t)(H1 + R) * LD + 3 * H0 + 2 * H1 + H0 + H1 + 4 * H1 + 4 * R + 2 * H0);
+      sizeof(float) * ((size_t)(H1 + R) * LD + 3 * H0 + 8 * H1 + H0 + H1 + 4 * H1 + 4 * R + 2 * H0);
 };
 
 template <int R>
@@ -494,8 +504,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   float* W4s = smem;               // [32][68]
   float* A0s = W4s + H1 * LD;      // [R][68]
   float* cf = A0s + R * LD;        // mean[64] alpha[64] beta[64]
-  float* red = cf + 3 * H0;        // [64]
-  float* a0r = red + 2 * H1;       // [64] A0 of batch row 0
+  float* red = cf + 3 * H0;        // [4 waves][64]
+  float* a0r = red + 8 * H1;       // [64] A0 of batch row 0
   float* shl = a0r + H0;           // [32] moment shift = Z4 of batch row 0
   float* part = shl + H1;          // [4][32]
   float* rsc = part + 4 * H1;      // [NTH] replica-sum scratch
@@ -544,7 +554,6 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     cf[H0 + c] = inv * bn_g;
     cf[2 * H0 + c] = bn_be;
   }
-  if (threadIdx.x < 2 * H1) red[threadIdx.x] = 0.f;
   *reinterpret_cast<float4*>(W4s + (we0 >> 4) * LD + 4 * (we0 & 15)) = w4a;
   *reinterpret_cast<float4*>(W4s + (we1 >> 4) * LD + 4 * (we1 & 15)) = w4b;
   __syncthreads();
@@ -599,14 +608,15 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     }
   }
   if (a.train) {
-    cols_to_lds<2>(s1, red);
-    cols_to_lds<2>(s2, red + H1);
+    cols_to_lds<2>(s1, red, 2 * H1);
+    cols_to_lds<2>(s2, red + H1, 2 * H1);
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) store_tile_rm_wt(T.Z4 + r0 * H1, 16 * w * H1 + 16 * j, H1, acc[j]);
   if (a.train) {
     __syncthreads();
-    if (threadIdx.x < 2 * H1) atomicAdd(&T.st1[rep_of_block() * 2 * H1 + threadIdx.x], red[threadIdx.x]);
+    if (threadIdx.x < 2 * H1)
+      xblock_add(a.det, T.st1, 2 * H1, T.dslot, 2 * H1, threadIdx.x, wave_rows_sum<4>(red, 2 * H1, threadIdx.x));
   }
   TT_STAMP(1, 4);
 }
@@ -652,10 +662,11 @@ struct TopLds {
   // fp32 region (float units)
   static constexpr int rsc = (dUi + 3 * PW) / 2;  // [4R] replica-sum scratch (phase 0), dU region after W8oth
   static constexpr int b8s = hend / 2;            // [2][DP] b8 of oth | own (0 for d >= D)
+  static constexpr int NW = R / 16;
   static constexpr int cf1 = b8s + 2 * DP;        // [2][4][H1] BN1 mean | gamma*inv | beta | inv per tower
-  static constexpr int red = cf1 + 8 * H1;        // [2*H1] dgamma1 | dbeta1 block partials
-  static constexpr int scal = red + 2 * H1;       // [0] loss part [1] dls part
-  static constexpr int rst = scal + 4;            // [2][2*H1] BN1 moment sums S1|S2 per tower
+  static constexpr int red = cf1 + 8 * H1;        // [NW][2*H1] dgamma1 | dbeta1 partials per wave
+  static constexpr int scal = red + NW * 2 * H1;  // [NW][2] (loss, dls) partials per wave
+  static constexpr int rst = scal + 2 * NW;       // [2][2*H1] BN1 moment sums S1|S2 per tower
   static constexpr int total = rst + 4 * H1;      // floats
   static_assert(3 * PW + 8 * R <= 3 * PU, "W8oth + rsc inside the dU region");
   static_assert(A1i % 8 == 0 && dUi % 8 == 0 && hend % 8 == 0, "16-B aligned images");
@@ -774,7 +785,6 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
     smem[L::b8s + threadIdx.x] = ok ? bo : 0.f;
     smem[L::b8s + DP + threadIdx.x] = ok ? bs : 0.f;
   }
-  if (threadIdx.x < 2 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;  // red + scal
   // W8 images: 3 bf16 planes of [DP][LDW], rows d >= D zero
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
@@ -935,8 +945,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
   if (own == 0) {  // loss + logit_scale grad once per row tile (lane group 0 covers the rows)
     const float lp = row_reduce16(loss_p), dp = row_reduce16(ds * sc);
     if (l == 0) {
-      atomicAdd(smem + L::scal + 0, lp);
-      atomicAdd(smem + L::scal + 1, dp);
+      smem[L::scal + 2 * w + 0] = lp;
+      smem[L::scal + 2 * w + 1] = dp;
     }
   }
 
@@ -1013,8 +1023,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
   for (int e = 0; e < 8; ++e) {
     const float vg = row_reduce16(sg[e]), vb = row_reduce16(dy[e]);
     if (r == 0) {
-      atomicAdd(smem + L::red + 8 * g + e, vg);
-      atomicAdd(smem + L::red + H1 + 8 * g + e, vb);
+      smem[L::red + w * 2 * H1 + 8 * g + e] = vg;
+      smem[L::red + w * 2 * H1 + H1 + 8 * g + e] = vb;
     }
   }
   __syncthreads();  // dU image, BN partials
@@ -1062,14 +1072,15 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
   }
   TT_STAMP(2, 6);
 
-  if (threadIdx.x < H1) {
-    atomicAdd(&T.gg1[rep_of_block() * BNG + threadIdx.x], smem[L::red + threadIdx.x]);
-    atomicAdd(&T.gbe1[rep_of_block() * BNG + threadIdx.x], smem[L::red + H1 + threadIdx.x]);
-  }
-  if (own == 0 && threadIdx.x == 0) {
-    float* lr = a.lsr + rep_of_block() * LSR;
-    atomicAdd(lr, smem[L::scal + 1]);
-    if (a.mode == TOP_TRAIN) atomicAdd(lr + 1, smem[L::scal + 0] / (float)a.B);
+  // dgamma1 | dbeta1 (adjacent in a replica) and (dls, loss): the waves'
+  // partials in wave order, then the cross-block accumulation
+  if (threadIdx.x < 2 * H1)
+    xblock_add(a.det, T.gg1, BNG, T.dslot, 2 * H1, threadIdx.x, wave_rows_sum<NW>(smem + L::red, 2 * H1, threadIdx.x));
+  if (own == 0 && threadIdx.x < 2) {
+    const int c = threadIdx.x;  // 0: dL/dlogit_scale, 1: batch-mean loss
+    const float v = EMB ? 0.f : wave_rows_sum<NW>(smem + L::scal + 1 - c, 2, 0);  // EMB: no cosine, no scale
+    if (c == 0 || a.mode == TOP_TRAIN || a.det)
+      xblock_add(a.det, a.lsr, LSR, a.dslot_lsr, 2, c, c == 0 ? v : (a.mode == TOP_TRAIN ? v / (float)a.B : 0.f));
   }
   TT_STAMP(2, 7);
 }
@@ -1109,9 +1120,9 @@ struct PairLds {
   // fp32 region (float units)
   static constexpr int b8s = hend / 2;              // [tower][DP] (0 for d >= D)
   static constexpr int cf1 = b8s + 2 * DP;          // [tower][4][H1] mean | gamma*inv | beta | inv
-  static constexpr int red = cf1 + 8 * H1;          // [tower][2*H1] dgamma1 | dbeta1 partials
-  static constexpr int scal = red + 4 * H1;         // [0] loss part [1] dls part
-  static constexpr int rsc = scal + 4;              // [512] replica-sum scratch
+  static constexpr int red = cf1 + 8 * H1;          // [8 waves][2*H1] dgamma1 | dbeta1 partials (tower = w >> 2)
+  static constexpr int scal = red + 16 * H1;        // [4 waves][2] (loss, dls) partials of the tower-0 waves
+  static constexpr int rsc = scal + 8;              // [512] replica-sum scratch
   static constexpr int rst = rsc + 512;             // [tower][2*H1] BN1 moment sums
   static constexpr int total = rst + 4 * H1;
 };
@@ -1170,7 +1181,6 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
   RepSum2<NTH, 2 * H1> rs;
   rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
   if (threadIdx.x < 2 * DP) smem[L::b8s + threadIdx.x] = (threadIdx.x % DP) < (unsigned)D ? b8v : 0.f;
-  if (threadIdx.x < 4 * H1 + 4) smem[L::red + threadIdx.x] = 0.f;  // red + scal
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
     const int e = (int)threadIdx.x + k * NTH, tt = e / WF4, el = e - tt * WF4;
@@ -1294,8 +1304,8 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
     if (a.score && g == 0 && valid) a.score[row] = sc;
     const float lp = row_reduce16(loss_p), dp = row_reduce16(ds * sc);
     if (l == 0) {
-      atomicAdd(smem + L::scal + 0, lp);
-      atomicAdd(smem + L::scal + 1, dp);
+      smem[L::scal + 2 * w + 0] = lp;
+      smem[L::scal + 2 * w + 1] = dp;
     }
   }
   const float dc = ds * s;
@@ -1350,8 +1360,8 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
   for (int e = 0; e < 8; ++e) {
     const float vg = row_reduce16(sg[e]), vb = row_reduce16(dy[e]);
     if (r == 0) {
-      atomicAdd(smem + L::red + tw * 2 * H1 + 8 * g + e, vg);
-      atomicAdd(smem + L::red + tw * 2 * H1 + H1 + 8 * g + e, vb);
+      smem[L::red + w * 2 * H1 + 8 * g + e] = vg;
+      smem[L::red + w * 2 * H1 + H1 + 8 * g + e] = vb;
     }
   }
   __syncthreads();  // W8 and exchange regions dead
@@ -1371,15 +1381,17 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
   __syncthreads();  // dU images, BN partials
   // BN1 affine and logit_scale / loss partials into the replicas, issued here
   // so their round trip overlaps dW8 instead of ending the kernel
+  // (dgamma1 | dbeta1 of a tower: the sum of its 4 waves' rows in wave order;
+  // adjacent in a replica)
   if (threadIdx.x < 4 * H1) {
     const int tt = (int)threadIdx.x / (2 * H1), k = (int)threadIdx.x % (2 * H1);
-    float* dst = k < H1 ? pick(tt, a.tw[0].gg1, a.tw[1].gg1) : pick(tt, a.tw[0].gbe1, a.tw[1].gbe1);
-    atomicAdd(&dst[rep_of_block() * BNG + (k % H1)], smem[L::red + threadIdx.x]);
+    const float v = wave_rows_sum<4>(smem + L::red + tt * 4 * 2 * H1, 2 * H1, k);
+    xblock_add(a.det, pick(tt, a.tw[0].gg1, a.tw[1].gg1), BNG, pick(tt, a.tw[0].dslot, a.tw[1].dslot), 2 * H1, k, v);
   }
-  if (threadIdx.x == 0) {
-    float* lr = a.lsr + rep_of_block() * LSR;
-    atomicAdd(lr, smem[L::scal + 1]);
-    atomicAdd(lr + 1, smem[L::scal + 0] / (float)a.B);
+  if (threadIdx.x < 2) {
+    const int c = threadIdx.x;  // 0: dL/dlogit_scale, 1: batch-mean loss
+    const float v = wave_rows_sum<4>(smem + L::scal + 1 - c, 2, 0);
+    xblock_add(a.det, a.lsr, LSR, a.dslot_lsr, 2, c, c == 0 ? v : v / (float)a.B);
   }
   TT_STAMP(2, 5);
 
@@ -1435,7 +1447,7 @@ struct MidLds {
   static constexpr int LDW = H0 + 4;   // W4 row-major [32][68]
   static constexpr int LDT = R + 4;    // transposed images [col][row]
   static constexpr size_t bytes =
-      sizeof(float) * ((size_t)H1 * LDW + (size_t)(H1 + H0) * LDT + H1 + 5 * H1 + 4 * H0 + 2 * H0 + 4 * R +
+      sizeof(float) * ((size_t)H1 * LDW + (size_t)(H1 + H0) * LDT + 4 * H1 + 5 * H1 + 4 * H0 + 8 * H0 + 4 * R +
                        2 * H1);
 };
 
@@ -1453,11 +1465,11 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   float* W4s = smem;                  // [32][68]  W4 row-major
   float* dZT = W4s + H1 * LDW;        // [32][R+4] dZ4^T
   float* A0T = dZT + H1 * LDT;        // [64][R+4] A0^T
-  float* db4 = A0T + H0 * LDT;        // [32]
-  float* c1 = db4 + H1;               // k1[32] mb[32] mg[32] mean1[32] inv1[32]
+  float* db4 = A0T + H0 * LDT;        // [4 waves][32]
+  float* c1 = db4 + 4 * H1;           // k1[32] mb[32] mg[32] mean1[32] inv1[32]
   float* c0 = c1 + 5 * H1;            // mean0[64] alpha0[64] beta0[64] inv0[64]
-  float* red = c0 + 4 * H0;           // [128]
-  float* rsc = red + 2 * H0;          // [NTH] replica-sum scratch
+  float* red = c0 + 4 * H0;           // [4 waves][128]
+  float* rsc = red + 8 * H0;          // [NTH] replica-sum scratch
   float* rst = rsc + NTH;             // [2*32] sum dgamma1 | sum dbeta1
   TT_STAMP(3, 0);
 
@@ -1500,8 +1512,6 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     c0[2 * H0 + c] = be0v;
     c0[3 * H0 + c] = f0inv;
   }
-  if (threadIdx.x < H1) db4[threadIdx.x] = 0.f;
-  if (threadIdx.x < 2 * H0) red[threadIdx.x] = 0.f;
   *reinterpret_cast<float4*>(W4s + (we0 >> 4) * LDW + 4 * (we0 & 15)) = w4a;
   *reinterpret_cast<float4*>(W4s + (we1 >> 4) * LDW + 4 * (we1 & 15)) = w4b;
   __syncthreads();
@@ -1522,7 +1532,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     }
     store_tile_T(dZT, LDT, 16 * q, 16 * w, dz[q]);
     const float cb = col_reduce(dz[q][0] + dz[q][1] + dz[q][2] + dz[q][3]);
-    if (g == 0) atomicAdd(db4 + col, cb);
+    if (g == 0) db4[w * H1 + col] = cb;
   }
   const bool drop = a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
@@ -1578,15 +1588,13 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     }
     store_tile_rm_wt(T.dY0 + r0 * H0, 16 * w * H0 + 16 * j, H0, dyv);
   }
-  cols_to_lds<4>(sg, red);
-  cols_to_lds<4>(sb, red + H0);
+  cols_to_lds<4>(sg, red, 2 * H0);
+  cols_to_lds<4>(sb, red + H0, 2 * H0);
   __syncthreads();
   TT_STAMP(3, 3);
-  if (threadIdx.x < H0) {
-    atomicAdd(&T.gg0[rep_of_block() * BNG + threadIdx.x], red[threadIdx.x]);
-    atomicAdd(&T.gbe0[rep_of_block() * BNG + threadIdx.x], red[H0 + threadIdx.x]);
-  }
-  if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = db4[threadIdx.x];
+  if (threadIdx.x < 2 * H0)  // gamma0 | beta0 grads (adjacent in a replica)
+    xblock_add(a.det, T.gg0, BNG, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<4>(red, 2 * H0, threadIdx.x));
+  if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = wave_rows_sum<4>(db4, H1, threadIdx.x);
   TT_STAMP(3, 4);
 }
 
@@ -1630,11 +1638,11 @@ struct FoldLds {
   static constexpr int imgs_f = 3 * img / 2;     // floats
   static_assert(IX >= dead, "X' image clear of the phase-2 operands (written during phase 2)");
   static_assert(dZi % 8 == 0 && W4i % 8 == 0, "16-B aligned images");
-  static constexpr int db4 = imgs_f;             // [32]
-  static constexpr int c1 = db4 + H1;            // k1 mb mg mean1 inv1 [5][32]
+  static constexpr int db4 = imgs_f;             // [8 waves][32]
+  static constexpr int c1 = db4 + 8 * H1;        // k1 mb mg mean1 inv1 [5][32]
   static constexpr int c0 = c1 + 5 * H1;         // mean0 alpha0 beta0 inv0 [4][64]
-  static constexpr int red = c0 + 4 * H0;        // sum dY0 Zh0 | sum dY0 | sum Zh0 | sum X' [4][64]
-  static constexpr int rsc = red + 4 * H0;       // [4R] replica-sum scratch
+  static constexpr int red = c0 + 4 * H0;        // [8 waves][sum dY0 Zh0 | sum dY0 | sum Zh0 | sum X' [4][64]]
+  static constexpr int rsc = red + 8 * 4 * H0;   // [4R] replica-sum scratch
   static constexpr int rst = rsc + 4 * R;        // [2][32] sum dgamma1 | sum dbeta1
   static constexpr int total = rst + 2 * H1;
   static constexpr size_t bytes = sizeof(float) * (size_t)total;
@@ -1728,8 +1736,6 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
       c0[3 * H0 + c] = f0inv;
     }
   }
-  if (threadIdx.x < H1) db4[threadIdx.x] = 0.f;
-  if (threadIdx.x < 4 * H0) red[threadIdx.x] = 0.f;
   put_planes4(hs + L::W4i + w4r * H1 + ((w4c ^ swz_dz(w4r)) * 4), L::PW4, w4v);
   __syncthreads();
   TT_STAMP(3, 1);
@@ -1773,7 +1779,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
       put_planes4(hs + L::dZi + zr * H1 + ((zc ^ swz_dz(zr)) * 4), L::PZ, make_float4(tq[0], tq[1], tq[2], tq[3]));
     }
     const float cb = col_reduce(dz[q][0] + dz[q][1] + dz[q][2] + dz[q][3]);
-    if (g == 0) atomicAdd(db4 + col, cb);
+    if (g == 0) db4[w * H1 + col] = cb;
   }
   const bool drop = a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
@@ -1885,16 +1891,16 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
 #pragma unroll
     for (int i = 0; i < 4; ++i) sx[i] = col_reduce(d[0][i] + d[1][i] + d[2][i] + d[3][i]);
     if (g == 0) {
-      float* rs = red + 3 * H0 + 4 * xc;
+      float* rs = red + w * 4 * H0 + 3 * H0 + 4 * xc;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(rs + i, sx[i]);
+      for (int i = 0; i < 4; ++i) rs[i] = sx[i];
     }
   }
   TT_STAMP(3, 4);
   TT_STAMP_T(4, 4, 448);
-  cols_to_lds<4>(sg, red);
-  cols_to_lds<4>(sb, red + H0);
-  cols_to_lds<4>(sz, red + 2 * H0);
+  cols_to_lds<4>(sg, red, 4 * H0);
+  cols_to_lds<4>(sb, red + H0, 4 * H0);
+  cols_to_lds<4>(sz, red + 2 * H0, 4 * H0);
   __syncthreads();  // every wave is past dW4 and dA0 (A0, dZ4, W4^T images)
   TT_STAMP(3, 5);
   TT_STAMP_T(4, 5, 448);
@@ -1963,14 +1969,10 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
     for (int j = 0; j < 4; ++j)
       if (j < KT) store_tile_rm_wt(slab, so + 32 * j, 2 * kp, acc[j]);
   }
-  if (threadIdx.x < H0) {
-    float* fr = T.fr + rep_of_block() * FRW;
-    atomicAdd(fr + threadIdx.x, red[threadIdx.x]);                    // gamma0 grad
-    atomicAdd(fr + H0 + threadIdx.x, red[H0 + threadIdx.x]);          // beta0 grad
-    atomicAdd(fr + 2 * H0 + threadIdx.x, red[2 * H0 + threadIdx.x]);  // sum Zh0
-    atomicAdd(fr + 3 * H0 + threadIdx.x, red[3 * H0 + threadIdx.x]);  // sum X'
-  }
-  if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = db4[threadIdx.x];
+  static_assert(FRW == 4 * H0, "fold replica: gamma0 grad | beta0 grad | sum Zh0 | sum X'");
+  if (threadIdx.x < 4 * H0)
+    xblock_add(a.det, T.fr, FRW, T.dslot, FRW, threadIdx.x, wave_rows_sum<8>(red, 4 * H0, threadIdx.x));
+  if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = wave_rows_sum<8>(db4, H1, threadIdx.x);
   TT_STAMP(3, 7);
   TT_STAMP_T(4, 7, 448);
 }
@@ -1987,7 +1989,7 @@ struct FirstLds {
     return a > b ? a : b;
   }
   static size_t bytes(int kp) {
-    return sizeof(float) * (xt_floats(kp) + (size_t)H0 * LDT + H0 + 5 * H0 + 2 * R + 4 * R + 2 * H0);
+    return sizeof(float) * (xt_floats(kp) + (size_t)H0 * LDT + 4 * H0 + 5 * H0 + 2 * R + 4 * R + 2 * H0);
   }
 };
 
@@ -2008,8 +2010,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   int64_t* ridx = reinterpret_cast<int64_t*>(smem);  // [R]
   float* XT = smem + 2 * R;                            // [kp][R+4]
   float* dZT = XT + FirstLds<R>::xt_floats(kp);        // [64][R+4]
-  float* db0 = dZT + H0 * LDT;                         // [64]
-  float* c0 = db0 + H0;                                // k0[64] mb[64] mg[64] mean0[64] inv0[64]
+  float* db0 = dZT + H0 * LDT;                         // [4 waves][64]
+  float* c0 = db0 + 4 * H0;                            // k0[64] mb[64] mg[64] mean0[64] inv0[64]
   float* rsc = c0 + 5 * H0;                            // [NTH] replica-sum scratch
   float* rst = rsc + NTH;                              // [2*64] sum dgamma0 | sum dbeta0
   TT_STAMP(4, 0);
@@ -2042,7 +2044,6 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     c0[2 * H0 + c] = a.train ? rst[c] * invB : 0.f;
     c0[3 * H0 + c] = f0mean;
     c0[4 * H0 + c] = f0inv;
-    db0[c] = 0.f;
   }
   __syncthreads();
   TT_STAMP(4, 1);
@@ -2124,7 +2125,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
     }
     store_tile_T(dZT, LDT, 16 * j, 16 * w, dz[j]);
     const float cb = col_reduce(dz[j][0] + dz[j][1] + dz[j][2] + dz[j][3]);
-    if (g == 0) atomicAdd(db0 + col, cb);
+    if (g == 0) db0[w * H0 + col] = cb;
   }
   __syncthreads();
   TT_STAMP(4, 2);
@@ -2188,6 +2189,10 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
         for (int i = 0; i < 4; ++i) {
           const int rl = 16 * w + 4 * g + i;
           if (r0 + rl >= a.B) continue;
+          if (a.det) {  // deterministic: the row's dX, scattered in row order by k_det_scatter
+            T.demb[(r0 + rl) * T.emb_w + c] = dx[0][i];
+            continue;
+          }
           int64_t code = T.cat[ridx[rl] * T.cat_ld + jj];
           code = code < 0 ? 0 : (code >= T.emb_rows[jj] ? T.emb_rows[jj] - 1 : code);
           atomicAdd(T.gemb[jj] + code * T.emb_dim + e, dx[0][i]);
@@ -2195,7 +2200,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
       }
     }
   }
-  if (threadIdx.x < H0) slab[T.so_b0 + threadIdx.x] = db0[threadIdx.x];
+  if (threadIdx.x < H0) slab[T.so_b0 + threadIdx.x] = wave_rows_sum<4>(db0, H0, threadIdx.x);
   TT_STAMP(4, 3);
 }
 

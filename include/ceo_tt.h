@@ -53,7 +53,19 @@ typedef struct tt_model_desc {
   float dropout_p;                     /* nn.Dropout(0.1) */
   float bn_eps;                        /* 1e-5 */
   float bn_momentum;                   /* 0.1 */
+  int32_t flags;                       /* TT_FLAG_* execution options */
 } tt_model_desc;
+
+/* tt_model_desc.flags
+ * TT_FLAG_DETERMINISTIC: bitwise repeatable steps.  Cross-block sums (BN
+ *   moments, BN-affine grads, the loss / logit_scale partials, the folded BN0
+ *   sums, embedding gradients) are accumulated by float atomics in arrival
+ *   order by default; with the flag every block stores its partial in a slot
+ *   of its own and a fold kernel adds the slots in block order (one extra
+ *   launch per reduction point).  The reference's CPU loop is repeatable
+ *   under torch.manual_seed (training.py:36-57); so is a fused step with
+ *   this flag.  The workspace layout does not depend on the flags.       */
+#define TT_FLAG_DETERMINISTIC 1
 
 /* One batch, described over dataset-resident arrays.  Row i of the batch is
  * dataset row rows[row0 + i] (or row0 + i when rows == NULL).  With cycle > 0

@@ -56,8 +56,9 @@ def test_header_constants_match_binding():
 
 
 def test_struct_sizes_match_header_layout():
-    # tt_model_desc: 7 int32 + 32 int32 + 3 floats; tt_batch: 11 8-byte fields
-    assert ctypes.sizeof(N.TTModelDesc) == 4 * (7 + 2 * N.TT_MAX_CAT + 3)
+    # tt_model_desc: 7 int32 + 32 int32 + 3 floats + flags; tt_batch: 11 8-byte fields
+    assert ctypes.sizeof(N.TTModelDesc) == 4 * (7 + 2 * N.TT_MAX_CAT + 3 + 1)
+    assert header_define("TT_FLAG_DETERMINISTIC") == N.TT_FLAG_DETERMINISTIC
     assert ctypes.sizeof(N.TTBatch) == 8 * 15
     assert ctypes.sizeof(N.TTAdamHP) == 16
 

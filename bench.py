@@ -535,6 +535,33 @@ def main():
     loss = tr.pop_loss_sum() / args.steps  # also raises if the peer exchange failed
     pairs = args.steps * B * world
     value = pairs / elapsed
+    det_ms = None
+    if world == 1 and graph is not None and not args.no_extras:
+        # the same step in deterministic-reduction mode (TT_FLAG_DETERMINISTIC:
+        # slots + in-order folds instead of float atomics): its cost, reported
+        # beside the headline (which runs the default atomic mode)
+        tr.deterministic = True
+        g_det = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step_fn()
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(g_det):
+            for _ in range(chunk):
+                step_fn()
+        g_det.replay()
+        torch.cuda.synchronize()
+        reps = max(1, args.steps // chunk)
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            g_det.replay()
+        torch.cuda.synchronize()
+        det_ms = 1e3 * (time.perf_counter() - t1) / (reps * chunk)
+        tr.deterministic = None
+        N.set_deterministic(tr.desc, tr.is_deterministic())  # the event pass below calls the C-ABI directly
+        del g_det
+        tr.pop_loss_sum(read=False)
 
     result = {
         "metric": "training pairs/sec (fused fwd+bwd+Adam, CEOFirmMatcher two-tower)",
@@ -552,6 +579,7 @@ def main():
                                            else ("gloo all-reduce" if pg is not None else "none"))),
                    "exchange_vs_collective_us": (getattr(getattr(tr, "peer", None), "timing_us", None))},
         "mean_loss": round(loss, 5),
+        "deterministic_ms_per_step": round(det_ms, 4) if det_ms is not None else None,
     }
 
     if not args.no_extras:

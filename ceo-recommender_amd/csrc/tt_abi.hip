@@ -565,7 +565,8 @@ static void det_fold(const StepArgs& a, const Plan& P, DetPoint pt, hipStream_t 
     }
   }
   if (pt == DET_TOP) add(a.dslot_lsr, a.lsr, P.n_tiles_top, 2);
-  hipLaunchKernelGGL(k_det_fold, dim3((unsigned)((wmax + 255) / 256), (unsigned)n), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(k_det_fold, dim3((unsigned)((wmax + DET_COLS - 1) / DET_COLS), (unsigned)n),
+                     dim3(DET_COLS * DET_GROUPS), 0, s, f);
 }
 
 template <bool EMB>

@@ -238,10 +238,9 @@ template __global__ void k_reduce_adam<false>(RedArgs);
 // Deterministic mode (TT_FLAG_DETERMINISTIC).  The tower kernels store each
 // block's partial of a cross-block accumulator into its own slot instead of
 // a float atomic into a replica; k_det_fold sums the slots of every column in
-// a fixed order (8 interleaved partial sums over the slots, combined as a
-// fixed tree) into replica 0 -- the replicas the consumers then add are that
-// sum and zeros, so every step is bitwise repeatable.  Up to 4 arrays per
-// launch (blockIdx.y).
+// a fixed order (a fixed summation tree over the slots) into replica 0 -- the
+// replicas the consumers then add are that sum and zeros, so every step is
+// bitwise repeatable.  Up to 4 arrays per launch (blockIdx.y).
 // ---------------------------------------------------------------------------
 struct DetFold {
   const float* src[4];
@@ -249,20 +248,30 @@ struct DetFold {
   int n_slots[4], width[4];
 };
 
-__global__ __launch_bounds__(256) void k_det_fold(DetFold f) {
+// Block (x, y): 32 columns of array y; thread (c, q) sums slots q, q + 8,
+// q + 16, ... of column c (4 independent chains), then the 8 partials of a
+// column are added in q order: a fixed summation tree for any timing.
+constexpr int DET_COLS = 32, DET_GROUPS = 8;
+__global__ __launch_bounds__(DET_COLS * DET_GROUPS) void k_det_fold(DetFold f) {
+  __shared__ float part[DET_GROUPS][DET_COLS];
   const int k = blockIdx.y;
-  const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const int w = f.width[k], n = f.n_slots[k];
-  if (c >= w) return;
-  const float* s = f.src[k] + c;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int i = 0;
+  const int cl = (int)threadIdx.x % DET_COLS, q = (int)threadIdx.x / DET_COLS;
+  const int c = (int)blockIdx.x * DET_COLS + cl;
+  const bool live = c < w;
+  const float* s = f.src[k] + (live ? c : 0);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int i = q, u = 0;
 #pragma unroll 4
-  for (; i + 8 <= n; i += 8)
+  for (; i < n; i += DET_GROUPS, u = (u + 1) & 3) acc[u] += s[(int64_t)i * w];
+  part[q][cl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (q == 0 && live) {
+    float v = part[0][cl];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] += s[(int64_t)(i + q) * w];
-  for (; i < n; ++i) acc[i & 7] += s[(int64_t)i * w];
-  f.dst[k][c] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    for (int g = 1; g < DET_GROUPS; ++g) v += part[g][cl];
+    f.dst[k][c] = v;
+  }
 }
 
 // Embedding-table gradients in deterministic mode (model.py:69,74 backward,

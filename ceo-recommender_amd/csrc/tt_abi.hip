@@ -9,6 +9,7 @@
 
 #include "tt_common.h"
 #include "tt_tower.hip"
+#include "tt_topgen.hip"
 #include "tt_optim.hip"
 #include "tt_comm.hip"
 #include "tt_cosine.hip"
@@ -32,6 +33,7 @@ constexpr size_t LDS_MAX = 160 * 1024;
 // ---------------------------------------------------------------------------
 struct Layout {
   int in_dim[2], kp[2], n_num[2];
+  int latent;
   int64_t emb_off[2][TT_MAX_CAT];
   int64_t slot[2][TT_SLOTS_PER_TOWER];
   int64_t ls;
@@ -69,6 +71,7 @@ static Layout make_layout(const tt_model_desc* d) {
       off = round_up(off + (int64_t)d->cat_counts[t][j] * d->emb_dim[t], 4);
     }
   const int D = d->latent;
+  L.latent = D;
   L.fold_ok = true;
   for (int t = 0; t < 2; ++t) {
     const int in = d->n_num[t] + d->n_cat[t] * d->emb_dim[t];
@@ -112,6 +115,7 @@ struct WsLayout {
   int64_t gacc;
   int64_t det[2], det_lsr;     // deterministic mode: per-block partial slots [n_tiles][DET_W] per tower, (dls, loss)
   int64_t demb[2];             // deterministic mode: embedding-column dX per batch row [rows][emb_w] (-1: none)
+  int64_t ug[2], dug[2];       // LATENT > 128: U / V and dU / dV [rows][Dp] (-1: none)
   int64_t total;  // floats
   int n_tiles;
 };
@@ -164,6 +168,11 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
     const int ew = L.in_dim[t] - L.n_num[t];
     W.demb[t] = ew > 0 ? take(rows * ew) : -1;
   }
+  for (int t = 0; t < 2; ++t) {
+    const bool gen = L.latent > 128;
+    W.ug[t] = gen ? take(rows * gen_dp(L.latent)) : -1;
+    W.dug[t] = gen ? take(rows * gen_dp(L.latent)) : -1;
+  }
   W.total = off;
   return W;
 }
@@ -188,6 +197,8 @@ static void set_lds_attrs() {
                         (const void*)k_bwd_mid<ROWS>, (const void*)k_bwd_mid_fold<FOLD_ROWS, true>,
                         (const void*)k_bwd_mid_fold<FOLD_ROWS, false>, (const void*)k_bwd_first<ROWS>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_top_gen_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_top_gen_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   });
 }
 
@@ -200,10 +211,13 @@ struct Plan {
   int n_tiles_top;  // k_top tiles
   int n_tiles_mid;  // k_bwd_mid tiles (FOLD_ROWS rows when the BN0 backward is folded)
   bool fold;        // BN0 backward folded into k_bwd_mid_fold (k_bwd_first not launched)
+  bool top_gen;     // LATENT > 128: the generic top (tt_topgen.hip) instead of k_top / k_top_pair
+  size_t lds_gen_fwd, lds_gen_bwd;
 };
 
 static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P) {
-  if (d->latent > 128) return TT_ERR_UNSUPPORTED;
+  if (d->latent > GEN_MAX_D) return TT_ERR_UNSUPPORTED;
+  P->top_gen = d->latent > 128;
   P->ndt = d->latent <= 64 ? 4 : 8;
   const int kpm = std::max(L.kp[0], L.kp[1]);
   if (kpm > MAX_KP) return TT_ERR_UNSUPPORTED;
@@ -237,8 +251,17 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   P->lds_pair = sizeof(float) * (size_t)(P->ndt == 4 ? PairLds<4>::total : PairLds<8>::total);
   P->lds_mid = P->fold ? FoldLds<FOLD_ROWS>::bytes : MidLds<ROWS>::bytes;
   P->lds_first = FirstLds<ROWS>::bytes(kpm);
+  P->lds_gen_fwd = gen_fwd_lds(d->latent);
+  P->lds_gen_bwd = gen_bwd_lds(d->latent);
+  if (P->top_gen) {  // 64-row top tiles (the W8 slabs of the generic backward)
+    P->top_pair = false;
+    P->top_rows = 64;
+    P->n_tiles_top = P->n_tiles;
+    P->lds_top = P->lds_pair = 0;
+  }
   (void)emb;
-  for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first, P->lds_pair})
+  for (size_t s : {P->lds_l0, P->lds_l4, P->lds_top, P->lds_mid, P->lds_first, P->lds_pair, P->lds_gen_fwd,
+                   P->lds_gen_bwd})
     if (s > LDS_MAX) return TT_ERR_UNSUPPORTED;
   return TT_OK;
 }
@@ -325,6 +348,8 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
     T.dslot = ws + W.det[t];
     T.demb = W.demb[t] >= 0 ? ws + W.demb[t] : nullptr;
     T.emb_w = L.in_dim[t] - L.n_num[t];
+    T.ug = W.ug[t] >= 0 ? ws + W.ug[t] : nullptr;
+    T.dug = W.dug[t] >= 0 ? ws + W.dug[t] : nullptr;
     if (fold) {  // the folded k_bwd_mid accumulates gg0 | gbe0 into the fold replicas
       T.gg0 = T.fr;
       T.gbe0 = T.fr + H0;
@@ -564,7 +589,9 @@ static void det_fold(const StepArgs& a, const Plan& P, DetPoint pt, hipStream_t 
         add(T.dslot, T.gg0, P.n_tiles, 2 * H0);
     }
   }
-  if (pt == DET_TOP) add(a.dslot_lsr, a.lsr, P.n_tiles_top, 2);
+  // (the generic top's embedding backward writes no (dls, loss) slots: its
+  // replicas stay as the caller zeroed them)
+  if (pt == DET_TOP && !(P.top_gen && a.mode == TOP_EMB_BWD)) add(a.dslot_lsr, a.lsr, P.n_tiles_top, 2);
   hipLaunchKernelGGL(k_det_fold, dim3((unsigned)((wmax + DET_COLS - 1) / DET_COLS), (unsigned)n),
                      dim3(DET_COLS * DET_GROUPS), 0, s, f);
 }
@@ -582,6 +609,17 @@ static void launch_top_t(const StepArgs& a, const Plan& P, int grid_y, hipStream
     launch(k_top<8, 128, EMB>, grid, blk, P.lds_top, s, ev, a);
 }
 static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t s, Evs ev = {}) {
+  if (P.top_gen) {  // LATENT > 128 (tt_topgen.hip); no per-kernel events on this path
+    const dim3 g2(P.n_tiles, 2), g1(P.n_tiles), blk(GEN_NTH);
+    if (a.mode != TOP_EMB_BWD) hipLaunchKernelGGL(k_top_gen_fwd, g2, blk, P.lds_gen_fwd, s, a);
+    if (a.mode == TOP_FWD || a.mode == TOP_TRAIN || a.mode == TOP_BWD_GIVEN)
+      hipLaunchKernelGGL(k_cos_gen, g1, blk, 0, s, a);
+    if (a.mode == TOP_TRAIN || a.mode == TOP_BWD_GIVEN || a.mode == TOP_EMB_BWD)
+      hipLaunchKernelGGL(k_top_gen_bwd, g2, blk, P.lds_gen_bwd, s, a);
+    (void)grid_y;
+    (void)ev;
+    return;
+  }
   if (a.mode == TOP_TRAIN && P.top_pair) {
     if (P.ndt == 4)
       launch(k_top_pair<4>, dim3(P.n_tiles_top), dim3(512), P.lds_pair, s, ev, a);

@@ -353,6 +353,7 @@ struct TowerDev {
   float* dslot;
   float* demb;                            // det: dX of the embedding columns [Bpad][emb_w] for k_det_scatter
   int emb_w;                              // n_cat * emb_dim
+  float *ug, *dug;                        // LATENT > 128 (tt_topgen.hip): U (V) and dU (dV) [Bpad][Dp]
 };
 
 enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2, TOP_EMB_FWD = 3, TOP_EMB_BWD = 4 };

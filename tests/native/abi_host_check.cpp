@@ -94,7 +94,7 @@ int main() {
     if (d.n_num[0] > 0) CHECK(tt_forward(&d, p, p, nbt, &nob, 0, 0, 1, p, 1 << 30, p, nullptr) == TT_ERR_ARG);
   }
   // unsupported shapes
-  tt_model_desc big = desc(64, 64, {}, {}, 512);
+  tt_model_desc big = desc(64, 64, {}, {}, 1024);
   int32_t info[6];
   CHECK(tt_step_plan(&big, 16384, info, 6) == TT_ERR_UNSUPPORTED);
   tt_model_desc bad = desc(-1, 4, {}, {}, 8);

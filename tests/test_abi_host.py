@@ -153,7 +153,7 @@ def test_host_argument_errors():
     with pytest.raises(ValueError, match="Expected more than 1 value per channel when training"):
         N.check(rc, "tt_train_step", 1, 64)
     # unsupported geometry: LATENT_DIM beyond the fused top kernel
-    big = N.make_desc(desc.n_num, [[], []], desc.emb_dim, 512)
+    big = N.make_desc(desc.n_num, [[], []], desc.emb_dim, 1024)  # LATENT <= 512 (generic top, tt_topgen.hip)
     bb, keep2 = _batch(big, 64)
     assert fwd(big, bb, 0, 1 << 40) == N.TT_ERR_UNSUPPORTED
     # invalid descriptor (dropout p = 1, more categorical columns than supported)

@@ -574,7 +574,8 @@ def main():
                                f"bs={B}/GPU, dropout 0.1, Adam lr 4e-4",
                    "global_batch": B * world, "parallelism": f"dp{world}" if pg is not None else "single",
                    "graph": bool(graph is not None), "graph_chunk": chunk,
-                   "grad_exchange": ("peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
+                   "grad_exchange": ("peer-memory one-shot inside k_reduce_adam (+ Adam)" if tr.fused_exchange
+                                     else "peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
                                      else ("rccl all-reduce" if pg is not None and dist.get_backend(pg) == "nccl"
                                            else ("gloo all-reduce" if pg is not None else "none"))),
                    "exchange_vs_collective_us": (getattr(getattr(tr, "peer", None), "timing_us", None))},

@@ -67,10 +67,17 @@ class PeerExchange:
     gradients, times both, and returns None -- the caller keeps the
     collective -- unless every rank agrees the exchange is correct and faster.
     ``CEO_TT_PEER_AR=0`` disables it, ``=1`` skips the timing comparison
-    (and the one-rank-per-GPU requirement: tests only)."""
+    (and the one-rank-per-GPU requirement: tests only).  At world size 1
+    there is nothing to exchange: the region is mapped, the timing skipped,
+    and ``train_step`` is the single-GPU step (tests the N > 1 path).
 
-    def __init__(self, lib, regions, own, rank, world, n, device):
+    ``train_step`` runs a whole fused step with the exchange inside its
+    gradient reduction (tt_train_step_dp); ``run`` is the standalone
+    exchange + Adam launch after a step that stopped at the gradient."""
+
+    def __init__(self, lib, regions, own, rank, world, n, device, co_ranks=1):
         self.lib, self.rank, self.world, self.n, self.device = lib, rank, world, n, device
+        self.co_ranks = co_ranks  # ranks of this job on this rank's device (1: one process per GPU)
         self.regions, self.own = regions, own
         self.peers = N.TTArPeers()
         for q, r in enumerate(regions):
@@ -84,8 +91,10 @@ class PeerExchange:
     def create(n: int, group=None, device=None, mode: Optional[str] = None) -> "Optional[PeerExchange]":
         import os
         mode = os.environ.get("CEO_TT_PEER_AR", "auto") if mode is None else mode
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
         world = world_of(group)
-        if mode == "0" or world < 2 or world > N.TT_AR_MAX_RANKS:
+        if mode == "0" or world < 1 or world > N.TT_AR_MAX_RANKS:
             return None
         rank = dist.get_rank(group)
         flag_dev = device if dist.get_backend(group) == "nccl" else "cpu"
@@ -108,6 +117,8 @@ class PeerExchange:
         if int(ok.item()) == 0:
             return None
         ex = PeerExchange._map(n, group, device, rank, world)  # every rank joins its collectives
+        if ex is not None:
+            ex.co_ranks = sum(1 for w in where if w == where[rank])
         ok.fill_(int(ex is not None))
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # every rank mapped, or none uses it
         if int(ok.item()) == 0:
@@ -118,7 +129,7 @@ class PeerExchange:
         try:
             if not ex._check(group):
                 use.zero_()
-            elif mode != "1" and not ex._faster_than_collective(group):
+            elif mode != "1" and world > 1 and not ex._faster_than_collective(group):
                 use.zero_()
         except Exception:  # noqa: BLE001
             use.zero_()
@@ -212,6 +223,19 @@ class PeerExchange:
                                            ptr(exp_avg_sq), hp, ptr(state), int(step_host), self.err.data_ptr(),
                                            int(self.wait_us), N.stream_ptr(self.device))
         N.check(rc, "tt_ar_allreduce_adam")
+
+    def train_step(self, tr, batch) -> int:
+        """One fused data-parallel step of FusedTrainer ``tr`` on ``batch``
+        (tt_train_step_dp); returns the library's status --
+        TT_ERR_UNSUPPORTED (nothing launched) when the reduction's blocks
+        cannot all be resident, which the trainer answers with the
+        two-launch form."""
+        a = tr.arena
+        return self.lib.tt_train_step_dp(tr.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
+                                         batch, tr.hp, tr.seed, tr.state.data_ptr(), tr.ws.data_ptr(), tr.ws_bytes,
+                                         tr.grad.data_ptr(), tr.exp_avg.data_ptr(), tr.exp_avg_sq.data_ptr(),
+                                         ctypes.byref(self.peers), self.rank, self.world, self.co_ranks,
+                                         self.err.data_ptr(), int(self.wait_us), N.stream_ptr(self.device))
 
     def failed(self) -> bool:
         """True once any exchange on this rank timed out (reads err: syncs)."""

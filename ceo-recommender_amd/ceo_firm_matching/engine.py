@@ -6,11 +6,14 @@ call (``tt_train_step``): no per-step host sync, no ``.item()``, no per-sample
 collate.  The dataset lives in HBM; a batch is a slice of a row-index
 permutation that the first kernel gathers from.
 
-Data parallel (one process per GPU, ``torch.distributed`` over RCCL): the
-step stops after the gradient reduction (``apply_adam=0``), the flat fp32
-gradient is all-reduced (AVG, one call per step), and ``tt_adam_apply``
-finishes the step -- DistributedDataParallel semantics with per-rank
-(local) BatchNorm statistics.
+Data parallel (one process per GPU, ``torch.distributed`` over RCCL) --
+DistributedDataParallel semantics with per-rank (local) BatchNorm
+statistics: with the peer-memory exchange (``distributed.PeerExchange``) the
+mean over ranks happens inside the step's last kernel (``tt_train_step_dp``:
+the gradient reduction publishes, waits for the peers and applies Adam);
+otherwise the step stops after the gradient reduction (``apply_adam=0``), the
+flat fp32 gradient is all-reduced (AVG, one call per step), and
+``tt_adam_apply`` finishes the step.
 """
 from __future__ import annotations
 
@@ -57,7 +60,15 @@ class FusedTrainer:
             broadcast_state_(self.arena.params, self.arena.buffers, process_group)
         # one-launch gradient exchange + Adam over peer memory when every rank
         # can map it and it beats the collective (else the RCCL all-reduce)
-        self.peer = PeerExchange.create(n, process_group, dev) if self.world > 1 else None
+        self.peer = PeerExchange.create(n, process_group, dev) if self.dp else None
+        # exchange inside the step's reduction (None: not tried yet).  Only
+        # with one rank per GPU: a rank spinning in its reduction holds LDS and
+        # wave slots that a co-located rank's forward kernels need, so ranks
+        # sharing a device (rehearsals) keep the two-launch form unless
+        # CEO_TT_FUSED_EX=1 (tests with small kernels)
+        import os
+        self.fused_exchange = None if self.peer is not None and (
+            self.peer.co_ranks == 1 or os.environ.get("CEO_TT_FUSED_EX") == "1") else False
         self.max_batch = 0
         self.ws = None
         self.ensure_batch(max_batch)
@@ -111,14 +122,30 @@ class FusedTrainer:
                                     self.exp_avg_sq.data_ptr(), int(apply_adam), N.stream_ptr(self.device))
         N.check(rc, "tt_train_step", n_rows, 64)
 
+    def _launch_dp(self, batch, n_rows):
+        """The data-parallel step: the exchange inside the step's reduction
+        when the peer exchange is mapped and the reduction's blocks can all be
+        resident (tt_train_step_dp; decided once), else reduce -> exchange
+        (peer launch or RCCL all-reduce) -> Adam."""
+        if self.peer is not None and self.fused_exchange is not False:
+            self.ensure_batch(n_rows)
+            N.set_deterministic(self.desc, self.is_deterministic())
+            rc = self.peer.train_step(self, batch)
+            if rc != N.TT_ERR_UNSUPPORTED:
+                N.check(rc, "tt_train_step_dp", n_rows, 64)
+                self.fused_exchange = True
+                return
+            self.fused_exchange = False
+        self._launch(batch, n_rows, False)
+        self.allreduce_and_adam()
+
     def step(self, rows: Optional[torch.Tensor], row0: int, n_rows: int):
         """One optimizer step on dataset rows rows[row0:row0+n_rows]."""
         batch = self._batch(rows, row0, n_rows)
         if not self.dp:
             self._launch(batch, n_rows, True)
         else:
-            self._launch(batch, n_rows, False)
-            self.allreduce_and_adam()
+            self._launch_dp(batch, n_rows)
             self._check_eager()
         self.steps_host += 1
 
@@ -130,8 +157,7 @@ class FusedTrainer:
         if not self.dp:
             self._launch(batch, batch_size, True)
         else:
-            self._launch(batch, batch_size, False)
-            self.allreduce_and_adam()
+            self._launch_dp(batch, batch_size)
             self._check_eager()
         self.steps_host += 1
 

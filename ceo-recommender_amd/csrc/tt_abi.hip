@@ -541,12 +541,25 @@ static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev
   if (a.fr_zero) return;
   launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
-static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}) {
-  if (r.adam_slots || !r.apply_adam)  // <true> reads no coefficients when there is no Adam
-    launch(k_reduce_adam<true>, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
+static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}, bool ex = false) {
+  const dim3 grid((unsigned)(r.vn / RED_E)), blk(RED_E * RED_G);
+  if (ex)  // data-parallel exchange inside the reduction (tt_train_step_dp: Adam slots set)
+    launch(k_reduce_adam<true, true>, grid, blk, 0, s, ev, r);
+  else if (r.adam_slots || !r.apply_adam)  // <true> reads no coefficients when there is no Adam
+    launch(k_reduce_adam<true, false>, grid, blk, 0, s, ev, r);
   else
-    launch(k_reduce_adam<false>, dim3((unsigned)(r.vn / RED_E)), dim3(RED_E * RED_G), 0, s, ev, r);
+    launch(k_reduce_adam<false, false>, grid, blk, 0, s, ev, r);
 }
+
+// ---- peer-memory exchange region (tt_ar_*): [flags of the standalone
+// exchange: TT_AR_MAX_RANKS x AR_BLOCKS][flags of the fused step:
+// TT_AR_MAX_RANKS x ar_red_blocks(n)][slot 0][slot 1] ----
+static constexpr int AR_BLOCKS = 32;
+static int64_t ar_slot_floats(int64_t n) { return (n + 63) / 64 * 64; }
+// k_reduce_adam blocks of any model with n parameters: every segment's
+// element range is at most 2 len + 64 long and starts on a block
+static int64_t ar_red_blocks(int64_t n) { return (2 * n) / RED_E + 2 * MAX_SEG + 1; }
+static int64_t ar_flag_bytes(int64_t n) { return (int64_t)TT_AR_MAX_RANKS * (AR_BLOCKS + ar_red_blocks(n)) * 8; }
 
 // Deterministic mode: fold the per-block partial slots the kernel of stage
 // `pt` just stored into replica 0 of each accumulator (k_det_fold), or
@@ -820,7 +833,8 @@ int32_t tt_embed_backward_ex(const tt_model_desc* d, const float* params, const 
 static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
                                const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws,
                                int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq, int32_t apply_adam,
-                               tt_stream_t stream, void* const* events) {
+                               tt_stream_t stream, void* const* events, const RedExchange* x = nullptr,
+                               int32_t co_ranks = 1) {
   if (!params || !buffers || !nbt || !state || !ws || !grad) return TT_ERR_ARG;
   if (apply_adam && (!hp || !exp_avg || !exp_avg_sq)) return TT_ERR_ARG;
   if (b && b->cycle > 0 && b->n_rows < 1) return TT_ERR_ARG;
@@ -829,6 +843,23 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
+  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
+  if (x) {
+    // every block of the reduction waits for its peers' same block: all of
+    // them (co_ranks grids when ranks share this device) must be resident at
+    // once, else the caller keeps the two-launch exchange
+    const int64_t blocks = r.vn / RED_E;
+    if (blocks > ar_red_blocks(c.L.n)) return TT_ERR_UNSUPPORTED;
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_reduce_adam<true, true>, RED_E * RED_G, 0) !=
+            hipSuccess)
+      return TT_ERR_UNSUPPORTED;
+    if (blocks * std::max(co_ranks, 1) > (int64_t)per_cu * cus) return TT_ERR_UNSUPPORTED;
+    r.x = *x;
+    r.x.blocks = (int32_t)ar_red_blocks(c.L.n);
+  }
   StepArgs a;
   fill_args(a, d, c.L, c.W, c.P.fold, params, buffers, nbt, b, w);
   a.train = 1;
@@ -861,7 +892,6 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   det_fold(a, c.P, DET_MID, s);
   launch_first(a, c.P, s, ev(4));
   det_fold(a, c.P, DET_FIRST, s);
-  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   r.inv_b = 1.f / (float)b->n_rows;
   for (int t = 0; t < 2; ++t) {
     r.zero_buf[2 * t] = w + c.W.st0[t];
@@ -882,7 +912,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     r.adam_slots = a.adam_slots;
     r.state = state;
   }
-  launch_reduce(r, s, ev(5));
+  launch_reduce(r, s, ev(5), x != nullptr);
   return launch_check();
 }
 
@@ -899,6 +929,31 @@ int32_t tt_train_step_ev(const tt_model_desc* d, float* params, float* buffers, 
                          void* const* events) {
   return train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg, exp_avg_sq,
                          apply_adam, stream, events);
+}
+
+int32_t tt_train_step_dp(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt, const tt_batch* b,
+                         const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws, int64_t ws_bytes,
+                         float* grad, float* exp_avg, float* exp_avg_sq, const tt_ar_peers* peers, int32_t rank,
+                         int32_t world, int32_t co_ranks, int32_t* err, int64_t wait_us, tt_stream_t stream) {
+  if (!peers || world < 1 || world > TT_AR_MAX_RANKS || rank < 0 || rank >= world || !err || co_ranks < 1 ||
+      !hp || !exp_avg || !exp_avg_sq || !desc_ok(d))
+    return TT_ERR_ARG;
+  const int64_t n = make_layout(d).n;
+  RedExchange x;
+  std::memset(&x, 0, sizeof(x));
+  for (int q = 0; q < world; ++q) {
+    if (!peers->region[q]) return TT_ERR_ARG;
+    char* base = (char*)peers->region[q];
+    x.flags[q] = (uint64_t*)(base + (int64_t)TT_AR_MAX_RANKS * AR_BLOCKS * 8);
+    x.slot[q] = (float*)(base + ar_flag_bytes(n));
+  }
+  x.slot_stride = ar_slot_floats(n);
+  x.rank = rank;
+  x.world = world;
+  x.err = err;
+  x.wait_ticks = (uint64_t)(wait_us > 0 ? wait_us : 2000000) * 100ull;  // s_memrealtime: 100 MHz
+  return train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg, exp_avg_sq, 1,
+                         stream, nullptr, &x, co_ranks);
 }
 
 int32_t tt_adam_apply(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
@@ -1364,14 +1419,11 @@ int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n
   return launch_check();
 }
 
-// ---- data-parallel gradient exchange over peer memory ----
-static constexpr int AR_BLOCKS = 32;
-static int64_t ar_flag_bytes() { return (int64_t)TT_AR_MAX_RANKS * AR_BLOCKS * 8; }
-static int64_t ar_slot_floats(int64_t n) { return (n + 63) / 64 * 64; }
-
+// ---- data-parallel gradient exchange over peer memory (region layout at
+// ar_flag_bytes above) ----
 int64_t tt_ar_region_bytes(int64_t n) {
   if (n < 1) return TT_ERR_ARG;
-  return ar_flag_bytes() + 2 * ar_slot_floats(n) * (int64_t)sizeof(float);
+  return ar_flag_bytes(n) + 2 * ar_slot_floats(n) * (int64_t)sizeof(float);
 }
 
 int32_t tt_ar_alloc(int64_t bytes, void** region, void* ipc_handle) {
@@ -1427,7 +1479,7 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
     if (!peers->region[q]) return TT_ERR_ARG;
     char* base = (char*)peers->region[q];
     a.flags[q] = (uint64_t*)base;
-    a.slot[q] = (float*)(base + ar_flag_bytes());
+    a.slot[q] = (float*)(base + ar_flag_bytes(n));
   }
   a.slot_stride = ar_slot_floats(n);
   a.rank = rank;

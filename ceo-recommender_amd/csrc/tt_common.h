@@ -719,6 +719,18 @@ struct Seg {
   const float *k0, *xsh; // kinds 3, 4: inv0*gamma0, shift row
 };
 
+// Data-parallel gradient exchange inside k_reduce_adam (tt_train_step_dp):
+// every rank's exchange region mapped here (tt_ar_*; flags of the fused step
+// [TT_AR_MAX_RANKS][blocks] after the standalone exchange's flags).
+struct RedExchange {
+  float* slot[TT_AR_MAX_RANKS];      // slot 0 of each rank's region (slot 1 at + slot_stride)
+  uint64_t* flags[TT_AR_MAX_RANKS];  // each rank's fused-step flag array
+  int64_t slot_stride;
+  int32_t rank, world, blocks;
+  int32_t* err;                      // set when a wait times out (sticky)
+  uint64_t wait_ticks;               // wait bound in s_memrealtime ticks (100 MHz)
+};
+
 struct RedArgs {
   Seg seg[MAX_SEG];
   int32_t n_seg;
@@ -741,6 +753,7 @@ struct RedArgs {
   tt_state* state;
   int64_t step_host;
   float inv_b;           // 1 / batch rows (kinds 3, 4)
+  RedExchange x;         // k_reduce_adam<PRE, true>: mean over ranks before Adam
 };
 
 }  // namespace tt

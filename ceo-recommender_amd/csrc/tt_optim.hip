@@ -4,7 +4,8 @@
 //   slabs (dW/db written by the tower kernels) in a fixed order -- or take the
 //   atomically accumulated value (BN affine, embeddings, logit_scale) -- write
 //   the full gradient, zero the accumulators for the next step, and optionally
-//   apply Adam in the same pass (single-GPU training: one launch for K10+K11).
+//   apply Adam in the same pass (single-GPU training: one launch for K10+K11);
+//   EX: the data-parallel mean over ranks (peer memory) between the two.
 // k_adam : Adam alone (data-parallel: after the RCCL all-reduce of `grad`).
 //
 // Adam arithmetic follows torch 2.10 _single_tensor_adam (optim.Adam.step,
@@ -26,12 +27,63 @@ namespace tt {
 // reads 64 B of one 128-B P|Q row segment.
 // PRE: the step's Adam coefficients come from the workspace cache (AdamSlot,
 // tt_common.h: a fused train step); otherwise the owner lanes compute them.
-template <bool PRE>
+// Data-parallel exchange of the reduced gradient (EX instance; all threads of
+// the block call it, owner lanes carry an element).  The one-shot protocol of
+// tt_comm.hip (k_ar_adam) per reduction block: publish this block's sums into
+// this rank's slot[t & 1], signal flag[rank][block] = t on every peer, wait
+// (bounded) for every peer's flag, then the mean in rank order -- this rank's
+// own term from the register, the same bits its slot holds, so every rank
+// computes bitwise the same mean.  World 1: nothing to exchange.  Returns
+// false (block-uniform) when the exchange is off (sticky err) or timed out:
+// the caller then leaves this block's parameters and Adam state untouched.
+// Slot reuse: rank r rewrites slot[t & 1] at step t + 2, after its step-t+1
+// block saw every peer's step-t+1 flag, which the peer wrote in a launch that
+// started after its step-t launch (the one reading slot[t & 1]) ended.
+__device__ __forceinline__ bool reduce_exchange(const RedExchange& X, int64_t t, bool owner, int64_t e, float& g,
+                                                int* ok_s) {
+  if (*ok_s == 0) return false;
+  if (X.world == 1) return true;
+  const uint64_t epoch = (uint64_t)t;
+  const int b = blockIdx.x, q = threadIdx.x;
+  const int64_t par = (t & 1) ? X.slot_stride : 0;
+  if (owner) __hip_atomic_store(X.slot[X.rank] + par + e, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // every wave's slot stores performed before the barrier that precedes the
+  // flags (explicit wait: the fence's own may be dropped, tt_comm.hip)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (q < X.world && q != X.rank) {
+    __hip_atomic_store(X.flags[q] + (int64_t)X.rank * X.blocks + b, epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t* f = X.flags[X.rank] + (int64_t)q * X.blocks + b;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > X.wait_ticks) {
+        *ok_s = 0;
+        atomicAdd(X.err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  if (*ok_s == 0) return false;
+  if (owner) {
+    float s = 0.f;
+    for (int r = 0; r < X.world; ++r)
+      s += r == X.rank ? g : __hip_atomic_load(X.slot[r] + par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    g = s * (1.0f / (float)X.world);
+  }
+  return true;
+}
+
+template <bool PRE, bool EX>
 __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedArgs a) {
   static_assert(NREP % RED_G == 0, "kinds 2-4: group pg takes replicas pg, pg + RED_G, ...");
   static_assert(RED_E % 32 == 0, "kind 3 pairs lanes el and el + 16 of a 32-lane group");
   __shared__ float part[RED_G][RED_E];
   __shared__ float xpart[4][RED_G][RED_E];  // kinds 3, 4: gg0, gbe0, sum Zh0, sum X' replicas
+  __shared__ int xok_s;                     // EX: exchange live (no earlier timeout on this rank)
   TT_STAMP(5, 0);
   // the step first: a later load would make its wait (in-order vmcnt) wait for the slabs
   // (a select of the two addresses: one FLAT load, issued first -- measured
@@ -182,38 +234,44 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
       if (a.loss_state) a.loss_state->loss_sum += l;
     }
   }
+  if (EX && threadIdx.x == 0) xok_s = __hip_atomic_load(a.x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
   __syncthreads();
   TT_STAMP(5, 1);
-  if (!owner) return;
+  if (!EX && !owner) return;
   float gsum = 0.f;
+  if (owner) {
 #pragma unroll
-  for (int k = 0; k < RED_G; ++k) gsum += part[k][el];
-  if (kind == 5) {  // then the second slab half of the same element (fixed order)
+    for (int k = 0; k < RED_G; ++k) gsum += part[k][el];
+    if (kind == 5) {  // then the second slab half of the same element (fixed order)
 #pragma unroll
-    for (int k = 0; k < RED_G; ++k) gsum += part[k][el + 32];
-  }
-  if (kind == 3 || kind == 4) {
-    // dW0 = k0 (P - mb s - mg Q) + db0 c,  db0 = -k0 mg sum Zh0  (k_bwd_mid_fold)
-    float gg = 0.f, zs = 0.f;
-#pragma unroll 4
-    for (int k = 0; k < RED_G; ++k) {
-      gg += xpart[0][k][el];
-      zs += xpart[2][k][el];
+      for (int k = 0; k < RED_G; ++k) gsum += part[k][el + 32];
     }
-    const float k0 = S.k0[ch], mg = gg * a.inv_b;
-    const float db0 = -k0 * mg * zs;  // = sum over rows of dZ0 (BN0 cancels b0: ~0)
-    if (kind == 3) {
-      float q = 0.f, gb = 0.f, sx = 0.f;
+    if (kind == 3 || kind == 4) {
+      // dW0 = k0 (P - mb s - mg Q) + db0 c,  db0 = -k0 mg sum Zh0  (k_bwd_mid_fold)
+      float gg = 0.f, zs = 0.f;
 #pragma unroll 4
       for (int k = 0; k < RED_G; ++k) {
-        q += part[k][el + 16];
-        gb += xpart[1][k][el];
-        sx += xpart[3][k][el];
+        gg += xpart[0][k][el];
+        zs += xpart[2][k][el];
       }
-      gsum = k0 * (gsum - (gb * a.inv_b) * sx - mg * q) + S.xsh[kx] * db0;
-    } else {
-      gsum = db0;
+      const float k0 = S.k0[ch], mg = gg * a.inv_b;
+      const float db0 = -k0 * mg * zs;  // = sum over rows of dZ0 (BN0 cancels b0: ~0)
+      if (kind == 3) {
+        float q = 0.f, gb = 0.f, sx = 0.f;
+#pragma unroll 4
+        for (int k = 0; k < RED_G; ++k) {
+          q += part[k][el + 16];
+          gb += xpart[1][k][el];
+          sx += xpart[3][k][el];
+        }
+        gsum = k0 * (gsum - (gb * a.inv_b) * sx - mg * q) + S.xsh[kx] * db0;
+      } else {
+        gsum = db0;
+      }
     }
+  }  // owner
+  if constexpr (EX) {
+    if (!reduce_exchange(a.x, t, owner, e, gsum, &xok_s) || !owner) return;
   }
   a.grad[e] = gsum;
   if (kind == 1) a.gacc[e] = 0.f;
@@ -231,8 +289,9 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   }
 }
 
-template __global__ void k_reduce_adam<true>(RedArgs);
-template __global__ void k_reduce_adam<false>(RedArgs);
+template __global__ void k_reduce_adam<true, false>(RedArgs);
+template __global__ void k_reduce_adam<false, false>(RedArgs);
+template __global__ void k_reduce_adam<true, true>(RedArgs);
 
 // ---------------------------------------------------------------------------
 // Deterministic mode (TT_FLAG_DETERMINISTIC).  The tower kernels store each

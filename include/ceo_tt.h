@@ -354,6 +354,23 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
                              float* exp_avg_sq, const tt_adam_hp* hp, tt_state* state,
                              int64_t step_host, int32_t* err, int64_t wait_us, tt_stream_t stream);
 
+/* One data-parallel training step with the exchange inside the gradient
+ * reduction (training.py:44-57 under DDP): tt_train_step's
+ * kernels, whose last one (k_reduce_adam) publishes each block's reduced
+ * gradient slice into this rank's region, signals the peers, waits (bounded)
+ * for theirs, takes the mean in rank order and applies Adam -- the launch and
+ * the boundary of tt_ar_allreduce_adam disappear.  Same peers / err / wait_us
+ * semantics as tt_ar_allreduce_adam (epoch = the device step counter), grad =
+ * the mean gradient.  co_ranks = ranks of this job sharing this device (1 for
+ * one process per GPU).  Returns TT_ERR_UNSUPPORTED with nothing launched
+ * when the reduction's blocks (co_ranks grids of them) cannot all be resident
+ * at once: the caller keeps tt_train_step(apply_adam=0) + tt_ar_allreduce_adam. */
+int32_t tt_train_step_dp(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
+                         const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state,
+                         void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
+                         const tt_ar_peers* peers, int32_t rank, int32_t world, int32_t co_ranks,
+                         int32_t* err, int64_t wait_us, tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -202,7 +202,8 @@ def test_exchange_timeout_leaves_parameters_and_raises():
 def _ddp_fold_rank(rank, world, port, q):
     """B = 8192 per rank on the cfg-3 model: the folded BN0 backward
     (k_bwd_mid_fold + the reduce's P/Q combine, apply_adam = 0) feeding the
-    peer exchange + Adam, vs the oracle's per-shard local-BN DDP step."""
+    peer exchange + Adam, vs the oracle's per-shard local-BN DDP step (ranks
+    sharing the GPU: the two-launch form)."""
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CEO_TT_PEER_AR="1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -259,3 +260,120 @@ def test_data_parallel_folded_step_on_peer_exchange():
         pytest.skip("no HIP device")
     for rank, err, where in _spawn(_ddp_fold_rank, 2):
         assert err < 1e-5, (rank, err, where)
+
+
+# ---- the exchange inside the step's gradient reduction (tt_train_step_dp) ----
+
+def _cfg2_model(dev, g):
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    cfg = Config()
+    cfg.LATENT_DIM = 64
+    cfg.DROPOUT_P = 0.1
+    cfg.DEVICE = dev
+    m = CEOFirmMatcher(meta_of(load_golden("cfg2")), cfg)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()})
+    return m.to(dev)
+
+
+def _fused_vs_two_launch_rank(rank, world, port, q, steps):
+    """K deterministic data-parallel steps with the exchange inside
+    k_reduce_adam vs the same steps as reduce -> standalone exchange + Adam
+    (fused_exchange forced off): bitwise the same parameters, Adam moments
+    and BN buffers; parameters and moments the same on every rank."""
+    import torch.distributed as dist
+    # CEO_TT_FUSED_EX: the in-reduction exchange although the ranks share the
+    # GPU (small kernels: the co-located ranks' steps still fit beside it)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CEO_TT_PEER_AR="1", CEO_TT_FUSED_EX="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching.engine import FusedTrainer
+        dev = torch.device("cuda:0")
+        g = load_golden("ddp")
+        shard = {k: torch.from_numpy(v) for k, v in sub(g, f"G2/shard{rank % 2}").items()}
+        B = shard["target"].shape[0]
+        outs = []
+        for fused in (True, False):
+            m = _cfg2_model(dev, g)
+            tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=5, process_group=dist.group.WORLD, deterministic=True)
+            assert tr.peer is not None
+            if not fused:
+                tr.fused_exchange = False
+            tr.set_data(shard)
+            for _ in range(steps):
+                tr.step(None, 0, B)
+            tr.pop_loss_sum()
+            assert tr.fused_exchange is fused, (fused, tr.fused_exchange)
+            outs.append(np.concatenate([tr.arena.params.cpu().numpy(), tr.exp_avg.cpu().numpy(),
+                                        tr.exp_avg_sq.cpu().numpy(), tr.arena.buffers.cpu().numpy()]))
+            tr.peer.close()
+        allo = [None] * world  # parameters and Adam moments (BN buffers are per rank: local statistics)
+        dist.all_gather_object(allo, outs[0][:3 * tr.arena.params.numel()].tobytes())
+        q.put((rank, bool(np.array_equal(outs[0], outs[1])), all(a == allo[0] for a in allo)))
+    except Exception as e:
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_exchange_inside_reduction_matches_two_launch_form(world):
+    """World 1 (bench --dp): the N > 1 step degenerates to the single-GPU
+    arithmetic; world 2 (two ranks on the test box's GPU): the in-reduction
+    exchange equals the standalone exchange bitwise, and every rank holds the
+    same parameters."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    for rank, same, ranks_equal in _spawn(_fused_vs_two_launch_rank, world, 3):
+        assert same is True, (rank, same)
+        assert ranks_equal is True, rank
+
+
+def test_exchange_inside_reduction_timeout_leaves_parameters():
+    """tt_train_step_dp with a peer that never runs: the reduction's waits
+    time out, parameters / Adam moments stay at their values (never an
+    update from the local gradient alone), later steps are device-side
+    no-ops for the exchange, and the host check raises."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ctypes
+    from ceo_firm_matching import _native as N
+    from ceo_firm_matching.distributed import PeerExchange
+    from ceo_firm_matching.engine import FusedTrainer
+    dev = torch.device("cuda:0")
+    g = load_golden("ddp")
+    m = _cfg2_model(dev, g)
+    tr = FusedTrainer(m, lr=4e-4, max_batch=64, seed=5)
+    L = N.lib()
+    n = tr.arena.params.numel()
+    nbytes = int(L.tt_ar_region_bytes(n))
+    regs = []
+    for _ in range(2):
+        r = ctypes.c_void_p()
+        h = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)()
+        N.check(L.tt_ar_alloc(nbytes, ctypes.byref(r), h), "tt_ar_alloc")
+        regs.append(r.value)
+    ex = PeerExchange(L, regs, regs[0], 0, 2, n, dev)
+    ex.regions = [regs[0], None]
+    ex.wait_us = 20_000
+    try:
+        tr.peer, tr.dp, tr.world, tr.fused_exchange = ex, True, 2, None
+        shard = {k: torch.from_numpy(v) for k, v in sub(g, "G2/shard0").items()}
+        tr.set_data(shard)
+        B = shard["target"].shape[0]
+        p0, m0, v0 = tr.arena.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone()
+        with pytest.raises(RuntimeError, match="did not publish"):
+            tr.step(None, 0, B)  # eager data-parallel steps check the exchange
+        assert tr.fused_exchange is True
+        assert torch.equal(tr.arena.params, p0) and torch.equal(tr.exp_avg, m0) and torch.equal(tr.exp_avg_sq, v0)
+        err1 = int(ex.err.item())
+        assert err1 > 0
+        with pytest.raises(RuntimeError, match="did not publish"):
+            tr.step(None, 0, B)
+        torch.cuda.synchronize()
+        assert int(ex.err.item()) == err1  # sticky: no new waits
+        assert torch.equal(tr.arena.params, p0)
+    finally:
+        torch.cuda.synchronize()
+        L.tt_ar_free(ctypes.c_void_p(regs[1]))
+        ex.close()

@@ -378,6 +378,7 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.lsr = ws + W.lsr;
   a.tgw = ws + W.tgw;
   a.det = (d->flags & TT_FLAG_DETERMINISTIC) ? 1 : 0;
+  a.xcd_pair = fold ? 1 : 0;  // 64-row tiles on the XCD of the fold kernel's 128-row tile (tile64)
   a.dslot_lsr = ws + W.det_lsr;
 }
 

@@ -443,7 +443,25 @@ struct StepArgs {
   float adam_lr, adam_b1, adam_b2, adam_eps;
   int det;               // deterministic reductions (TT_FLAG_DETERMINISTIC): slots + k_det_fold
   float* dslot_lsr;      // det: per-block (dls, loss) partials [blocks][2]
+  int xcd_pair;          // folded step: 64-row kernels take XCD-paired tiles (tile64)
 };
+
+// Row tile of a 64-row kernel's block (k_l0_fwd, k_l4_fwd, k_top_pair).
+// Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8;
+// each XCD has its own L2) and k_bwd_mid_fold's block x -- 128 rows, the
+// 64-row tiles 2x and 2x + 1 -- runs on XCD x % 8.  With xcd_pair the 64-row
+// kernels take their tiles so that 2x and 2x + 1 run on XCD x % 8 as well:
+// the Z0 / Z4 / dY1 tiles and X rows the fold kernel re-reads were last
+// touched through its own XCD's L2.  Bijective on every whole group of 16
+// tiles, identity on the rest.
+#ifndef TT_XCD_PAIR
+#define TT_XCD_PAIR 1
+#endif
+__device__ __forceinline__ int tile64(const StepArgs& a) {
+  const int b = blockIdx.x;
+  if (!TT_XCD_PAIR || !a.xcd_pair || b >= (a.n_tiles & ~15)) return b;
+  return 2 * (b & 7) + 16 * (b >> 4) + ((b >> 3) & 1);
+}
 
 // A block's partial sum of cross-block accumulator c: a float atomic into
 // replica rep_of_block() (order of arrival decides the rounding), or in

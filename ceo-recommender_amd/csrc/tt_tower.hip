@@ -347,7 +347,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
   const TowerDev& T = a.tw[t];
   const int64_t step = step_for_first_kernel(a);
   const int64_t base = batch_row0(a, step);
-  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int64_t r0 = (int64_t)tile64(a) * R;
   const int in = T.in_dim;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   uint16_t* Wh = reinterpret_cast<uint16_t*>(smem);
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   const int t = blockIdx.y;
   const TowerDev& T = a.tw[t];
   const int64_t step = step_current(a);
-  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int64_t r0 = (int64_t)tile64(a) * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   float* W4s = smem;               // [32][68]
   float* A0s = W4s + H1 * LD;      // [R][68]
@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
   const int64_t step = step_current(a);
-  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int64_t r0 = (int64_t)tile64(a) * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   const int tw = __builtin_amdgcn_readfirstlane(w >> 2);  // this wave's tower (uniform: scalar a.tw[tw] reads)
   const int rl = 16 * (w & 3) + r;   // this lane's row in the tile

@@ -15,7 +15,7 @@ fused step.  On CPU the reference loop runs with ATen ops.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.optim as optim
@@ -32,6 +32,62 @@ def sampler_batches(loader: DataLoader) -> List[List[int]]:
     the worker base seed first; the RandomSampler draws its seed lazily)."""
     torch.empty((), dtype=torch.int64).random_(generator=loader.generator)
     return [list(b) for b in loader.batch_sampler]
+
+
+def epoch_order_plan(loader: DataLoader, pin: bool = False) -> Optional[Callable[[], Tuple[torch.Tensor, List[int]]]]:
+    """One epoch's batch order of ``loader`` as ONE int64 index tensor (the
+    batches concatenated) and the batch sizes -- the order and global-RNG
+    consumption of ``sampler_batches`` without Python index lists (at 1M
+    pairs those took 80 ms per epoch, 25x the epoch's fused steps).
+
+    Consumes the global RNG now, exactly as ``iter(loader)`` does, and
+    returns a thunk that builds the order: for the default ``RandomSampler``
+    (its own generator seeded from that draw) the thunk depends on nothing
+    else, so epochs' permutations can be built on worker threads.  Covers the
+    samplers ``DataLoader(shuffle=...)`` builds (torch 2.10 ``RandomSampler``
+    without replacement over the whole dataset, or ``SequentialSampler``)
+    under the default ``BatchSampler``; None for any other sampler (the
+    caller then uses ``sampler_batches``).  ``pin``: the thunk returns the
+    order in pinned host memory (for an asynchronous upload)."""
+    from torch.utils.data import BatchSampler, RandomSampler, SequentialSampler
+    bsamp = loader.batch_sampler
+    if type(bsamp) is not BatchSampler:
+        return None
+    samp = bsamp.sampler
+    n = len(loader.dataset)
+    if type(samp) is RandomSampler:
+        if samp.replacement or samp.num_samples != n or len(samp.data_source) != n:
+            return None
+    elif type(samp) is not SequentialSampler:
+        return None
+    bs = bsamp.batch_size
+    sizes = [bs] * (n // bs)
+    if n % bs and not bsamp.drop_last:
+        sizes.append(n % bs)
+    total = sum(sizes)
+    torch.empty((), dtype=torch.int64).random_(generator=loader.generator)  # the iterator's base seed
+    if type(samp) is SequentialSampler:
+        return lambda: (torch.arange(total, dtype=torch.int64), sizes)
+    if samp.generator is not None:
+        # a caller-owned generator: its draws are sequential, made now (the
+        # exhausted iterator's trailing randperm(n)[:0] advances it too)
+        order = torch.randperm(n, generator=samp.generator)
+        torch.randperm(n, generator=samp.generator)
+        return lambda: (order[:total], sizes)
+    seed = int(torch.empty((), dtype=torch.int64).random_().item())  # RandomSampler.__iter__
+
+    def build():
+        gen = torch.Generator()
+        gen.manual_seed(seed)
+        order = torch.randperm(n, generator=gen)[:total]
+        return (order.pin_memory() if pin else order), sizes
+    return build
+
+
+def epoch_order(loader: DataLoader) -> Optional[Tuple[torch.Tensor, List[int]]]:
+    """``epoch_order_plan`` built at once: (order, batch sizes) or None."""
+    plan = epoch_order_plan(loader)
+    return None if plan is None else plan()
 
 
 def _resident_data(loader: DataLoader) -> Optional[Dict[str, torch.Tensor]]:
@@ -59,6 +115,72 @@ def train_model(train_loader: DataLoader, val_loader: DataLoader,
 train = train_model  # the north-star name
 
 
+# epochs whose batch order is built ahead on worker threads (one thread and
+# one pinned order each: 80 MB at 10M pairs); 6 keeps the 10M-pair epoch's
+# permutation (0.23 s per thread) near the device's 33 ms of steps per epoch
+_ORDER_AHEAD = 6
+
+
+class _EpochSteps:
+    """An epoch's full batches as hipGraph replays.  The epoch's order lives
+    in one persistent device buffer (refilled before each epoch, stream
+    ordered), batch j of every epoch is rows[j*bs : (j+1)*bs], and the steps
+    run in cycle mode: cycle = the epoch's step count (the partial batch, a
+    host-mode step, takes the last slot), t_base = the device step counter at
+    the start of training, so the batch index ((t-1-t_base) % cycle) is j in
+    every epoch and the captured launches replay unchanged.  Epoch 0 runs
+    eagerly (first launches load the kernels); the graphs, chunks of 16 steps
+    (the bench's measured best), are captured after it.  Any capture failure
+    keeps eager cycle-mode steps."""
+
+    CHUNK = 16
+
+    def __init__(self, trainer: FusedTrainer, rows: torch.Tensor, bs: int, n_full: int, cycle: int, t_base: int):
+        self.tr, self.rows, self.bs, self.n_full, self.cycle, self.t_base = trainer, rows, bs, n_full, cycle, t_base
+        self.graphs = None
+        self.eager = False
+
+    def _step(self):
+        self.tr.step_cycle(self.rows, self.bs, self.cycle, t_base=self.t_base)
+
+    def _capture(self):
+        try:
+            graphs = []
+            sizes = [self.CHUNK] * (self.n_full // self.CHUNK) + ([self.n_full % self.CHUNK] if self.n_full % self.CHUNK else [])
+            made = {}
+            for k in sizes:  # one graph per distinct chunk length
+                if k not in made:
+                    g = torch.cuda.CUDAGraph()
+                    # thread_local: the order workers pin host memory meanwhile
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):  # recorded only
+                        for _ in range(k):
+                            self._step()
+                    made[k] = g
+                graphs.append(made[k])
+            self.tr.steps_host -= sum(made)  # captured launches are not steps taken
+            self.graphs = graphs
+        except Exception:  # noqa: BLE001 -- capture unsupported here: eager steps
+            self.eager = True
+            import ctypes
+            try:  # the failed capture's error stays pending for the next launch check
+                ctypes.CDLL("libamdhip64.so").hipGetLastError()
+            except OSError:
+                pass
+
+    def run(self, epoch: int):
+        if epoch == 0 or self.eager:
+            for _ in range(self.n_full):
+                self._step()
+            return
+        if self.graphs is None:
+            self._capture()
+            if self.eager:
+                return self.run(epoch)
+        for g in self.graphs:
+            g.replay()
+        self.tr.steps_host += self.n_full
+
+
 def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> CEOFirmMatcher:
     dev = model.logit_scale.device
     bs = loader.batch_size or 1
@@ -66,18 +188,59 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> C
     data = _resident_data(loader)
     if data is not None:
         trainer.set_data(data)
+    # the epochs' batch orders: global-RNG draws in epoch order, the
+    # permutations built on worker threads a few epochs ahead (torch.randperm
+    # of the reference's sampler is sequential: 23 ns per pair, 10x an
+    # epoch's fused steps), so the device rarely waits for the host
+    pool, ahead, depth = None, [], min(_ORDER_AHEAD, config.EPOCHS)
+    pin = torch.cuda.is_available()
+    plan = epoch_order_plan(loader, pin) if data is not None and config.EPOCHS > 0 else None
+    nxt = None
+    if plan is not None:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=depth)
+        ahead.append(pool.submit(plan))
+        for _ in range(1, depth):
+            ahead.append(pool.submit(epoch_order_plan(loader, pin)))
+        nxt = ahead.pop(0).result()
+    runner = None
+    if nxt is not None:
+        # DataLoader(shuffle=...) epochs all have the same batch sizes: full
+        # batches replayed from graphs (_EpochSteps), the partial one eager
+        sizes0 = nxt[1]
+        n_full = sum(1 for b in sizes0 if b == bs)
+        if n_full and sizes0[:n_full] == [bs] * n_full:
+            rows_dev = torch.empty(len(nxt[0]), dtype=torch.int64, device=dev)
+            runner = _EpochSteps(trainer, rows_dev, bs, n_full, len(sizes0), trainer.steps_done())
     for epoch in range(config.EPOCHS):
         model.train()
         n_batches = 0
         if data is not None:
-            batches = sampler_batches(loader)
-            flat = [i for b in batches for i in b]
-            rows = torch.tensor(flat, dtype=torch.int64).to(dev, non_blocking=True)
-            off = 0
-            for b in batches:
-                trainer.step(rows, off, len(b))
-                off += len(b)
-                n_batches += 1
+            if nxt is not None:
+                order, sizes = nxt
+            else:
+                batches = sampler_batches(loader)
+                order = torch.tensor([i for b in batches for i in b], dtype=torch.int64)
+                sizes = [len(b) for b in batches]
+            if runner is not None:
+                runner.rows.copy_(order, non_blocking=True)
+                runner.run(epoch)
+                for bsz in sizes[runner.n_full:]:  # the partial batch: host mode, the cycle's last slot
+                    trainer.step(runner.rows, runner.n_full * bs, bsz)
+                n_batches = len(sizes)
+            else:
+                rows = order.to(dev, non_blocking=True)
+                off = 0
+                for bsz in sizes:
+                    trainer.step(rows, off, bsz)
+                    off += bsz
+                    n_batches += 1
+            # keep `depth` epochs' orders in flight (host RNG only: the fused steps
+            # draw nothing from it); the next one is usually built already
+            if pool is not None:
+                if epoch + depth < config.EPOCHS:
+                    ahead.append(pool.submit(epoch_order_plan(loader, pin)))
+                nxt = ahead.pop(0).result() if ahead else None
         else:
             for batch in loader:
                 batch = {k: v.to(dev) for k, v in batch.items()}
@@ -89,6 +252,8 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> C
             print(f"Epoch {epoch}: Avg Train Loss = {avg_loss:.4f}")
         else:
             trainer.pop_loss_sum(read=False)
+    if pool is not None:
+        pool.shutdown()
     trainer.check_exchange()
     model._trainer = trainer  # keeps optimizer state reachable for callers/tests
     return model

@@ -75,6 +75,54 @@ def test_train_model_cli_pipeline_on_fused_engine():
     assert not bad, bad
 
 
+def test_train_model_graph_epochs_equal_host_mode_steps():
+    """train_model's epochs (full batches replayed from hipGraphs in cycle
+    mode, the partial batch in host mode, the next epoch's order drawn while
+    the device runs) against a plain loop of host-mode steps over the
+    DataLoader's batches: bitwise the same parameters and BN buffers in
+    deterministic mode, with dropout."""
+    _need_gpu()
+    from torch.utils.data import DataLoader
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    from ceo_firm_matching.data import CEOFirmDataset
+    from ceo_firm_matching.engine import FusedTrainer
+    from ceo_firm_matching.training import sampler_batches, train_model
+    from test_host_pipeline import cli_data
+    cfg = Config()
+    cfg.EPOCHS = 5
+    cfg.DROPOUT_P = 0.1
+    cfg.DEVICE = torch.device("cuda")
+    train, val = cli_data(cfg)
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        torch.manual_seed(77)
+        tl = DataLoader(CEOFirmDataset(train), batch_size=128, shuffle=True)
+        with contextlib.redirect_stdout(io.StringIO()):
+            model = train_model(tl, None, train, cfg)
+        a = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+        n_steps = model._trainer.steps_done()
+        torch.manual_seed(77)
+        tl = DataLoader(CEOFirmDataset(train), batch_size=128, shuffle=True)
+        m = CEOFirmMatcher(train, cfg).to(cfg.DEVICE)
+        tr = FusedTrainer(m, lr=cfg.LEARNING_RATE, max_batch=128)
+        tr.set_data({k: train[k] for k in ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target",
+                                           "weights")})
+        for _ in range(cfg.EPOCHS):
+            batches = sampler_batches(tl)
+            rows = torch.tensor([i for b in batches for i in b], dtype=torch.int64, device=cfg.DEVICE)
+            off = 0
+            for b in batches:
+                tr.step(rows, off, len(b))
+                off += len(b)
+        torch.cuda.synchronize()
+        assert tr.steps_done() == n_steps
+        for k, v in m.state_dict().items():
+            assert np.array_equal(v.detach().cpu().numpy(), a[k]), k
+    finally:
+        torch.use_deterministic_algorithms(prev)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

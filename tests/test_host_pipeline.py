@@ -165,3 +165,39 @@ def test_reference_top_level_names_importable():
         assert hasattr(P, name), name
     with pytest.raises(NotImplementedError):
         P.explain_model_shap(None, None)
+
+
+@pytest.mark.parametrize("shuffle,drop_last,gen,n,bs", [
+    (True, False, False, 1000, 64), (True, True, False, 1000, 64), (False, False, False, 1000, 64),
+    (True, False, True, 1024, 64), (True, True, True, 999, 1000), (True, False, False, 7, 16)])
+def test_epoch_order_matches_the_dataloader(shuffle, drop_last, gen, n, bs):
+    """training.epoch_order (tensor batch order, no Python index lists) gives
+    the DataLoader's batches and leaves the global RNG -- and a loader
+    generator -- where iterating the loader does, epoch after epoch."""
+    from torch.utils.data import DataLoader, TensorDataset
+    from ceo_firm_matching.training import epoch_order_plan, sampler_batches
+    ds = TensorDataset(torch.arange(n))
+
+    def make():
+        g = torch.Generator().manual_seed(5) if gen else None
+        return DataLoader(ds, batch_size=bs, shuffle=shuffle, drop_last=drop_last, generator=g)
+
+    la, lb = make(), make()
+    torch.manual_seed(11)
+    ref = [sampler_batches(la) for _ in range(3)]
+    st_ref = torch.get_rng_state()
+    g_ref = la.generator.get_state() if gen else None
+    torch.manual_seed(11)
+    plans = [epoch_order_plan(lb) for _ in range(3)]  # drawn in order, built later in any order
+    got = [p() for p in plans[::-1]][::-1]
+    assert torch.equal(torch.get_rng_state(), st_ref)
+    if gen:
+        assert torch.equal(lb.generator.get_state(), g_ref)
+    for batches, (order, sizes) in zip(ref, got):
+        assert sizes == [len(b) for b in batches]
+        assert order.tolist() == [i for b in batches for i in b]
+    # and the same as iterating the DataLoader itself
+    torch.manual_seed(11)
+    lc = make()
+    it = [[int(x) for x in b[0]] for b in lc]
+    assert it == [list(b) for b in ref[0]]

@@ -138,10 +138,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // lines for the boundary's L2 write-back (MI355X_MICROARCH.md 'boundary':
 // + B / 6 TB/s when a kernel leaves B bytes dirty).  base must be uniform
 // across the wave (it becomes the SGPR buffer descriptor); off = per-lane bytes.
+template <int AUX = 16>
 __device__ __forceinline__ void st_wt16(const float* base, uint32_t off, f32x4 v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (int)off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (int)off, 0, AUX);
 }
+// Cache policy of the activation hand-offs (Z0, Z4, dY1) that the next
+// kernels re-read on the SAME XCD (tile64): 16 = sc1 (write-through, line
+// dropped), 0 = plain (kept in L2, written back at the boundary)
+#ifndef TT_HANDOFF_AUX
+#define TT_HANDOFF_AUX 16
+#endif
 
 __device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
 __device__ __forceinline__ float bf16_val(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
@@ -262,10 +269,11 @@ __device__ __forceinline__ f32x4 quad_transpose(f32x4 v) {
 // write-through store per lane (4 consecutive columns of one row).
 // base: block-uniform pointer; off: element offset of the tile's (0, 0) from
 // base (small); ld: row stride in floats (multiple of 4, base 16-B aligned).
+template <int AUX = 16>
 __device__ __forceinline__ void store_tile_rm_wt(const float* base, int off, int ld, f32x4 acc) {
   const int l = lane_id(), r = l & 15, g = l >> 4;
   const f32x4 t = quad_transpose(acc);
-  st_wt16(base, (uint32_t)((off + (4 * g + (r & 3)) * ld + (r & ~3)) * 4), t);
+  st_wt16<AUX>(base, (uint32_t)((off + (4 * g + (r & 3)) * ld + (r & ~3)) * 4), t);
 }
 // sum over the 4 lane groups (g = l>>4) that share a column r
 __device__ __forceinline__ float col_reduce(float v) { return xrow32_add(xrow16_add(v)); }

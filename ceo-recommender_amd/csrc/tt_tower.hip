@@ -451,7 +451,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
   // Z0 (workspace rows are padded to whole tiles: no guard), row-major via
   // quad transposes, 16-B write-through stores
 #pragma unroll
-  for (int j = 0; j < 4; ++j) store_tile_rm_wt(T.Z0 + r0 * H0, 16 * w * H0 + 16 * j, H0, acc[j]);
+  for (int j = 0; j < 4; ++j) store_tile_rm_wt<TT_HANDOFF_AUX>(T.Z0 + r0 * H0, 16 * w * H0 + 16 * j, H0, acc[j]);
   if (t == 0 && a.target && threadIdx.x < R) {  // (target, weight) of the tile's rows for k_top
     const int64_t drt = data_row(a, base, min(r0 + (int64_t)threadIdx.x, a.B - 1));
     *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + threadIdx.x)) = make_float2(a.target[drt], a.weight[drt]);
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     cols_to_lds<2>(s2, red + H1, 2 * H1);
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) store_tile_rm_wt(T.Z4 + r0 * H1, 16 * w * H1 + 16 * j, H1, acc[j]);
+  for (int j = 0; j < 2; ++j) store_tile_rm_wt<TT_HANDOFF_AUX>(T.Z4 + r0 * H1, 16 * w * H1 + 16 * j, H1, acc[j]);
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H1)
@@ -1016,8 +1016,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
   }
   {
     const uint32_t off = (uint32_t)((row * H1 + 8 * g) * 4);
-    st_wt16(T.dY1, off, f32x4{dy[0], dy[1], dy[2], dy[3]});
-    st_wt16(T.dY1, off + 16, f32x4{dy[4], dy[5], dy[6], dy[7]});
+    st_wt16<TT_HANDOFF_AUX>(T.dY1, off, f32x4{dy[0], dy[1], dy[2], dy[3]});
+    st_wt16<TT_HANDOFF_AUX>(T.dY1, off + 16, f32x4{dy[4], dy[5], dy[6], dy[7]});
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1353,8 +1353,8 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
   }
   {
     const uint32_t off = (uint32_t)((row * H1 + 8 * g) * 4);
-    st_wt16(T.dY1, off, f32x4{dy[0], dy[1], dy[2], dy[3]});
-    st_wt16(T.dY1, off + 16, f32x4{dy[4], dy[5], dy[6], dy[7]});
+    st_wt16<TT_HANDOFF_AUX>(T.dY1, off, f32x4{dy[0], dy[1], dy[2], dy[3]});
+    st_wt16<TT_HANDOFF_AUX>(T.dY1, off + 16, f32x4{dy[4], dy[5], dy[6], dy[7]});
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {

@@ -381,6 +381,17 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = T.b0[16 * j + r];
   const float bsh = T.b0[16 * w + r];
+  // (target, weight) of this lane's row for the top kernel (tower-0 blocks
+  // store them at the end): issued last, from the row index the lane already
+  // holds, unconditionally (valid dummy address without a target) -- no
+  // index load and no load chain at the end of the kernel (was 1.1-1.3 us)
+  const bool tgw_on = a.target != nullptr;
+  const float tg_v = (tgw_on ? a.target : T.b0)[tgw_on ? dr : 0];
+#ifdef TT_DIAG_TW_SAME  // timing probe: both values from one array (one line per row)
+  const float wt_v = (tgw_on ? a.target : T.b0)[tgw_on ? dr : 0] + 1.f;
+#else
+  const float wt_v = (tgw_on ? a.weight : T.b0)[tgw_on ? dr : 0];
+#endif
   // W0 image: zero columns >= in, split, store
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
@@ -452,10 +463,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
   // quad transposes, 16-B write-through stores
 #pragma unroll
   for (int j = 0; j < 4; ++j) store_tile_rm_wt<TT_HANDOFF_AUX>(T.Z0 + r0 * H0, 16 * w * H0 + 16 * j, H0, acc[j]);
-  if (t == 0 && a.target && threadIdx.x < R) {  // (target, weight) of the tile's rows for k_top
-    const int64_t drt = data_row(a, base, min(r0 + (int64_t)threadIdx.x, a.B - 1));
-    *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + threadIdx.x)) = make_float2(a.target[drt], a.weight[drt]);
-  }
+  if (t == 0 && tgw_on && g == 0)  // rows r0 + 16 w + r: the whole tile (tgw is padded to whole tiles)
+    *reinterpret_cast<float2*>(a.tgw + 2 * (r0 + 16 * w + r)) = make_float2(tg_v, wt_v);
   if (a.state && blockIdx.x == 0 && t == 0 && threadIdx.x == 0) a.state->step_cur = step;
   // Adam's coefficients for this step: normally cached by the previous
   // step's k_reduce_adam (AdamSlot); recomputed here when the slot does not

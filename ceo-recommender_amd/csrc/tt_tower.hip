@@ -385,13 +385,12 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
   // store them at the end): issued last, from the row index the lane already
   // holds, unconditionally (valid dummy address without a target) -- no
   // index load and no load chain at the end of the kernel (was 1.1-1.3 us)
+  // (tower-1 blocks read one shared line instead: the random gather is
+  // tower 0's alone)
   const bool tgw_on = a.target != nullptr;
-  const float tg_v = (tgw_on ? a.target : T.b0)[tgw_on ? dr : 0];
-#ifdef TT_DIAG_TW_SAME  // timing probe: both values from one array (one line per row)
-  const float wt_v = (tgw_on ? a.target : T.b0)[tgw_on ? dr : 0] + 1.f;
-#else
-  const float wt_v = (tgw_on ? a.weight : T.b0)[tgw_on ? dr : 0];
-#endif
+  const int64_t tgr = tgw_on && t == 0 ? dr : 0;
+  const float tg_v = (tgw_on ? a.target : T.b0)[tgr];
+  const float wt_v = (tgw_on ? a.weight : T.b0)[tgr];
   // W0 image: zero columns >= in, split, store
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {

@@ -306,8 +306,9 @@ __host__ __device__ __forceinline__ uint64_t dropout_key(uint64_t seed, uint64_t
 // element with bit HB clear takes its low 16 bits, the other the high 16;
 // keep iff that 16-bit uniform >= floor(p * 2^16).  HB follows how the
 // kernels hold a layer's columns, so both halves of a hash land in one lane:
-// layer 0 (A0, MFMA C layout: columns 16 apart) HB = 4, layer 1 (A1, k_top:
-// 8 consecutive columns per lane) HB = 0.  Two elements per permutation (two
+// layer 0 (A0: k_l4_fwd's A operand holds columns 8g.. and 32 + 8g.., the
+// backward kernels' MFMA C layout columns 16j + r, j = 0..3) HB = 5, layer 1
+// (A1, k_top: 8 consecutive columns per lane) HB = 0.  Two elements per permutation (two
 // quarter-rate multiplies each) halves the cost of recomputing the masks
 // wherever the forward or backward needs them.
 __host__ __device__ __forceinline__ uint32_t perm32(uint32_t x) {
@@ -328,7 +329,7 @@ __device__ __forceinline__ bool dropout_keep_rk(uint32_t rk, int col, uint32_t t
   const uint32_t h = perm32(rk ^ (pid * 0x9E3779B9u));
   return (((c >> HB) & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
 }
-constexpr int DROP_HB0 = 4, DROP_HB1 = 0;  // layer 0 (A0), layer 1 (A1)
+constexpr int DROP_HB0 = 5, DROP_HB1 = 0;  // layer 0 (A0), layer 1 (A1)
 
 // ---------------------------------------------------------------------------
 // Kernel argument block (passed by value; lives in the kernarg segment).

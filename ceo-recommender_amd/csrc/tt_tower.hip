@@ -490,55 +490,64 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
 
 // ---------------------------------------------------------------------------
 // k_l4_fwd : A0 = Drop(ReLU(BN0(Z0))) ; Z4 = A0 W4^T + b4 ; BN1 sums
+//
+// Z4 = A0 W4^T on the bf16x3 MFMA core with the A operand straight from
+// registers: lane (r, g) of wave w loads the Z0 slices it supplies as the A
+// operand of v_mfma_f32_16x16x32_bf16 -- row 16w + r, columns 8g .. 8g + 7
+// (K step 0) and 32 + 8g .. (K step 1) -- applies BN0 / ReLU / dropout and
+// splits them into planes in place: no A0 tile in LDS, no barrier between the
+// activation and the GEMM.  The dropout pair of layer 0 is (c, c + 32)
+// (DROP_HB0 = 5): both halves of every permutation are this lane's.  W4 is
+// staged once per block as bf16 planes (the B operand, l0's padded layout).
 // ---------------------------------------------------------------------------
 template <int R>
 struct L4Lds {
-  static constexpr int LD = H0 + 4;
-  static constexpr size_t bytes =
-      sizeof(float) * ((size_t)(H1 + R) * LD + 3 * H0 + 8 * H1 + H0 + H1 + 4 * H1 + 4 * R + 2 * H0);
+  static constexpr int LDK = H0 + 16;  // bf16 row stride of the W4 image (32-B pad: conflict-free reads)
+  static constexpr int PL = H1 * LDK;  // one W4 plane
+  // W4 planes [3][32][LDK] (bf16) | cf [3][64] | red [4][64] | a0r [64] | shl [32] | rsc [NTH] | rst [128]
+  static constexpr int f_cf = 3 * PL / 2;
+  static constexpr int f_red = f_cf + 3 * H0;
+  static constexpr int f_a0r = f_red + 8 * H1;
+  static constexpr int f_shl = f_a0r + H0;
+  static constexpr int f_rsc = f_shl + H1;
+  static constexpr int f_rst = f_rsc + 4 * R;
+  static constexpr size_t bytes = sizeof(float) * ((size_t)f_rst + 2 * H0);
+  static_assert(PL % 8 == 0, "16-B aligned planes");
 };
 
 template <int R>
 __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) {
-  constexpr int NTH = R * 4;
-  constexpr int LD = L4Lds<R>::LD;
-  constexpr int Z4PT = R * (H0 / 4) / NTH;  // float4 of Z0 per thread
+  using L = L4Lds<R>;
+  constexpr int NTH = R * 4, LDK = L::LDK, PL = L::PL;
+  static_assert(R == 64 && NTH == 256 && H0 == 64 && H1 == 32, "4 waves x 16 rows, two 32-deep K steps");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
   const TowerDev& T = a.tw[t];
   const int64_t step = step_current(a);
   const int64_t r0 = (int64_t)tile64(a) * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  float* W4s = smem;               // [32][68]
-  float* A0s = W4s + H1 * LD;      // [R][68]
-  float* cf = A0s + R * LD;        // mean[64] alpha[64] beta[64]
-  float* red = cf + 3 * H0;        // [4 waves][64]
-  float* a0r = red + 8 * H1;       // [64] A0 of batch row 0
-  float* shl = a0r + H0;           // [32] moment shift = Z4 of batch row 0
-  float* part = shl + H1;          // [4][32]
-  float* rsc = part + 4 * H1;      // [NTH] replica-sum scratch
-  float* rst = rsc + NTH;          // [2*64] BN0 moment sums S1|S2
+  uint16_t* Wh = reinterpret_cast<uint16_t*>(smem);  // W4 planes
+  float* cf = smem + L::f_cf;                        // mean[64] alpha[64] beta[64]
+  float* red = smem + L::f_red;                      // [4 waves][64]
+  float* a0r = smem + L::f_a0r;                      // [64] A0 of batch row 0
+  float* shl = smem + L::f_shl;                      // [32] moment shift = Z4 of batch row 0
+  float* rsc = smem + L::f_rsc;                      // [NTH] replica-sum scratch
+  float* rst = smem + L::f_rst;                      // [2*64] BN0 moment sums S1|S2
   TT_STAMP(1, 0);
 
-  // issue every load of the phase first (Z0 rows are padded: no clamp needed)
-  // (row-coalesced float4s: the two columns of a dropout hash pair sit in
-  // different lanes here, each lane evaluates its own -- measured cheaper
-  // than a pair-per-lane mapping's less coalesced Z0 reads)
-  float4 z[Z4PT];
-#pragma unroll
-  for (int k = 0; k < Z4PT; ++k) {
-    const int e = threadIdx.x + k * NTH;
-    const int rl = e >> 4, c4 = (e & 15) * 4;
-    z[k] = *reinterpret_cast<const float4*>(T.Z0 + (r0 + rl) * H0 + c4);
-  }
+  // ---- issue every load of the phase first (Z0 rows are padded: no clamp)
+  // this lane's A-operand slices of Z0: row 16w + r, columns 8g.. and 32 + 8g..
+  const float* zr = T.Z0 + (r0 + 16 * w + r) * H0 + 8 * g;
+  const float4 za0 = *reinterpret_cast<const float4*>(zr), za1 = *reinterpret_cast<const float4*>(zr + 4);
+  const float4 zb0 = *reinterpret_cast<const float4*>(zr + 32), zb1 = *reinterpret_cast<const float4*>(zr + 36);
   float bias[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias[j] = T.b4[16 * j + r];
   const float z0r_raw = T.Z0[min((int)threadIdx.x, H0 - 1)];
   const float z0r = threadIdx.x < H0 ? z0r_raw : 0.f;
   // W4 (raw) and wave 0's BN0 parameters are issued with the Z0 loads: one
-  // round trip for the whole phase (they used to follow the replica sum)
-  static_assert(H1 * H0 / 4 == 2 * NTH && H0 == 64, "W4: 2 float4 per thread; BN0: wave 0");
+  // round trip for the whole phase
+  static_assert(H1 * H0 / 4 == 2 * NTH, "W4: 2 float4 per thread; BN0: wave 0");
   const int we0 = (int)threadIdx.x, we1 = (int)threadIdx.x + NTH;  // two float4 per thread (named: no array)
   const float4 w4a = *reinterpret_cast<const float4*>(T.W4 + (we0 >> 4) * H0 + 4 * (we0 & 15));
   const float4 w4b = *reinterpret_cast<const float4*>(T.W4 + (we1 >> 4) * H0 + 4 * (we1 & 15));
@@ -552,50 +561,100 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     bn_g = T.g0[l];
     bn_be = T.be0[l];
   }
+  const bool drop = a.train && a.drop_thr > 0;
+  const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
   if (a.train) rep_sum<NTH, 2 * H0>(T.st0, 2 * H0, rsc, rst);
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
     float mean, inv;
     bn_coefs_pre(a, H0, rst, bn_sh, bn_rm, bn_rv, T.rm0, T.rv0, T.nbt0, T.fin0, a.update_stats && blockIdx.x == 0,
                  c, &mean, &inv);
+    const float alpha = inv * bn_g;
     cf[c] = mean;
-    cf[H0 + c] = inv * bn_g;
+    cf[H0 + c] = alpha;
     cf[2 * H0 + c] = bn_be;
+    // A0 of the batch's row 0 (the BN1 moment shift's input), bitwise as the
+    // tile rows compute it
+    if (a.train)
+      a0r[c] = bn_relu_drop(z0r, mean, alpha, bn_be, drop, dropout_row_key(key, 0), c, a.drop_thr, a.drop_scale);
   }
-  *reinterpret_cast<float4*>(W4s + (we0 >> 4) * LD + 4 * (we0 & 15)) = w4a;
-  *reinterpret_cast<float4*>(W4s + (we1 >> 4) * LD + 4 * (we1 & 15)) = w4b;
+  put_planes4(Wh + (we0 >> 4) * LDK + 4 * (we0 & 15), PL, w4a);
+  put_planes4(Wh + (we1 >> 4) * LDK + 4 * (we1 & 15), PL, w4b);
   __syncthreads();
   TT_STAMP(1, 1);
 
-  const bool drop = a.train && a.drop_thr > 0;
-  const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
+  // ---- A0 of this lane's 16 elements (columns c = 8g + e and c + 32), split
+  // into the two K steps' A operands
+  bf16x8 xa[2][3];
+  {
+    const f32x4* cv = reinterpret_cast<const f32x4*>(cf + 8 * g);
+    const f32x4 mu[4] = {cv[0], cv[1], cv[8], cv[9]};
+    const f32x4 al[4] = {cv[H0 / 4], cv[H0 / 4 + 1], cv[H0 / 4 + 8], cv[H0 / 4 + 9]};
+    const f32x4 be[4] = {cv[H0 / 2], cv[H0 / 2 + 1], cv[H0 / 2 + 8], cv[H0 / 2 + 9]};
+    const float zz[16] = {za0.x, za0.y, za0.z, za0.w, za1.x, za1.y, za1.z, za1.w,
+                          zb0.x, zb0.y, zb0.z, zb0.w, zb1.x, zb1.y, zb1.z, zb1.w};
+    float y[16];
 #pragma unroll
-  for (int k = 0; k < Z4PT; ++k) {
-    const int e = threadIdx.x + k * NTH;
-    const int rl = e >> 4, c4 = (e & 15) * 4;
-    const uint32_t rk = dropout_row_key(key, r0 + rl);
-    float4 o;
-    o.x = bn_relu_drop(z[k].x, cf[c4 + 0], cf[H0 + c4 + 0], cf[2 * H0 + c4 + 0], drop, rk, c4 + 0, a.drop_thr, a.drop_scale);
-    o.y = bn_relu_drop(z[k].y, cf[c4 + 1], cf[H0 + c4 + 1], cf[2 * H0 + c4 + 1], drop, rk, c4 + 1, a.drop_thr, a.drop_scale);
-    o.z = bn_relu_drop(z[k].z, cf[c4 + 2], cf[H0 + c4 + 2], cf[2 * H0 + c4 + 2], drop, rk, c4 + 2, a.drop_thr, a.drop_scale);
-    o.w = bn_relu_drop(z[k].w, cf[c4 + 3], cf[H0 + c4 + 3], cf[2 * H0 + c4 + 3], drop, rk, c4 + 3, a.drop_thr, a.drop_scale);
-    *reinterpret_cast<float4*>(A0s + rl * LD + c4) = o;
+    for (int e = 0; e < 16; ++e) {
+      const float v = (zz[e] - mu[e >> 2][e & 3]) * al[e >> 2][e & 3] + be[e >> 2][e & 3];
+      y[e] = v > 0.f ? v : 0.f;
+    }
+    if (drop) {  // pair (c, c + 32): low half of the permutation for c, high for c + 32
+      const uint32_t rk = dropout_row_key(key, r0 + 16 * w + r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t h = perm32(rk ^ ((uint32_t)(8 * g + e) * 0x9E3779B9u));
+        y[e] = (h & 0xFFFFu) >= a.drop_thr ? y[e] * a.drop_scale : 0.f;
+        y[8 + e] = (h >> 16) >= a.drop_thr ? y[8 + e] * a.drop_scale : 0.f;
+      }
+    }
+    float x0[8], x1[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x0[e] = y[e];
+      x1[e] = y[8 + e];
+    }
+    split8x3(x0, xa[0]);
+    split8x3(x1, xa[1]);
   }
-  if (a.train && threadIdx.x < H0) {
-    const int c = threadIdx.x;
-    a0r[c] = bn_relu_drop(z0r, cf[c], cf[H0 + c], cf[2 * H0 + c], drop, dropout_row_key(key, 0), c, a.drop_thr,
-                          a.drop_scale);
-  }
-  __syncthreads();
   TT_STAMP(1, 2);
 
-  if (a.train) {  // shift for the BN1 moment sums (see k_l0_fwd)
-    row_dot<NTH>(a0r, W4s, LD, H0, H1, T.b4, part, shl);
-    if (blockIdx.x == 0 && threadIdx.x < H1) T.shift1[threadIdx.x] = shl[threadIdx.x];
+  // ---- Z4 = A0 W4^T (bf16x3, two K steps per 16-column tile); waves 0 and 1
+  // also compute tile w of the shift row with the same MFMA sequence in every
+  // block (bitwise one shift for all blocks)
+  f32x4 acc[2] = {zero4(), zero4()}, accs = zero4();
+  {
+    bf16x8 sa[2][3];
+    if (a.train && w < 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const f32x4* ap = reinterpret_cast<const f32x4*>(a0r + 32 * kk + 8 * g);
+        const f32x4 p0 = ap[0], p1 = ap[1];
+        const float xs[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
+        split8x3(xs, sa[kk]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bf16x8 wf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          wf[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * j + r) * LDK + 32 * kk + 8 * g);
+        mfma_x3(xa[kk], wf, acc[j]);
+        if (a.train && j == w) mfma_x3(sa[kk], wf, accs);
+      }
+    }
   }
-  f32x4 acc[2] = {zero4(), zero4()};
-  strip_gemm_nt<2>(A0s + 16 * w * LD, LD, W4s, LD, H0, acc);
-  __syncthreads();
+  if (a.train) {
+    if (w < 2 && g == 0) {
+      const float sh = accs[0] + bias[w];
+      shl[16 * w + r] = sh;
+      if (blockIdx.x == 0) T.shift1[16 * w + r] = sh;
+    }
+    __syncthreads();  // shl
+  }
   TT_STAMP(1, 3);
 
   float s1[2], s2[2];

@@ -120,8 +120,8 @@ def dropout_keep_mask(seed: int, step: int, tower: int, layer: int,
     cols = np.arange(width, dtype=np.uint32)
     # columns c and c ^ 2^hb share one hash (pair id = c without bit hb): the
     # low 16 bits for bit hb clear, the high 16 otherwise (tt_common.h
-    # dropout_keep_rk; hb = 4 for layer 0, 0 for layer 1)
-    hb = np.uint32(4 if layer == 0 else 0)
+    # dropout_keep_rk; hb = 5 for layer 0, 0 for layer 1)
+    hb = np.uint32(5 if layer == 0 else 0)
     pid = ((cols >> (hb + np.uint32(1))) << hb) | (cols & ((np.uint32(1) << hb) - np.uint32(1)))
     hi = ((cols >> hb) & np.uint32(1)).astype(bool)
     with np.errstate(over="ignore"):

@@ -128,9 +128,9 @@ def test_dropout_mask_statistics():
     m2 = O.dropout_keep_mask(42, 8, 1, 0, 4096, 64, 0.1)
     assert (m != m2).mean() > 0.1
     assert O.dropout_keep_mask(1, 1, 0, 0, 8, 8, 0.0).all()
-    # the two columns sharing one hash (16 apart in layer 0, adjacent in
+    # the two columns sharing one hash (32 apart in layer 0, adjacent in
     # layer 1) are independent draws: P(both kept) = 0.81
-    for layer, hb in ((0, 16), (1, 1)):
+    for layer, hb in ((0, 32), (1, 1)):
         m = O.dropout_keep_mask(42, 7, 0, layer, 8192, 64, 0.1)
         c = np.arange(64)
         lo = c[(c & hb) == 0]

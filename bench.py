@@ -22,6 +22,7 @@ Extra legs (rank 0, N=1 only for the CPU baseline):
   Dataset + DataLoader(shuffle=True)) on a 524,288-pair sample.
 """
 import argparse
+import gc
 import ctypes
 import json
 import math
@@ -583,87 +584,17 @@ def main():
         "deterministic_ms_per_step": round(det_ms, 4) if det_ms is not None else None,
     }
 
-    if not args.no_extras:
-        # ---- per-kernel HIP events on the launch stream (separate pass, K steps)
-        st = N.stream_ptr(dev)
-        # 2 events per kernel, stamped by the kernel's own dispatch
-        # (tt_train_step_ev -> hipExtLaunchKernelGGL): kernel-only durations
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(12)] for _ in range(args.steps)]
-        for row in evs:
-            for e in row:
-                e.record()  # materialise the hipEvent
-        torch.cuda.synchronize()
-        a = tr.arena
-        for k in range(args.steps):
-            arr = (ctypes.c_void_p * 12)(*[e.cuda_event for e in evs[k]])
-            batch = tr._batch(rows, 0, B, cycle=n_batches)
-            rc = tr.lib.tt_train_step_ev(tr.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
-                                         batch, tr.hp, tr.seed, tr.state.data_ptr(), tr.ws.data_ptr(),
-                                         tr.ws_bytes, tr.grad.data_ptr(), tr.exp_avg.data_ptr(),
-                                         tr.exp_avg_sq.data_ptr(), int(pg is None), st, arr)
-            N.check(rc, "tt_train_step_ev")
-            if pg is not None:
-                tr.allreduce_and_adam()
-        torch.cuda.synchronize()
-        plan = N.step_plan(tr.desc, B)
-        per = {}
-        for i, name in enumerate(KERNELS):
-            if name == "k_bwd_first" and plan["folded_bn0_backward"]:
-                continue  # not launched: its work runs inside k_bwd_mid (folded BN0 backward)
-            per[name] = sum(evs[k][2 * i].elapsed_time(evs[k][2 * i + 1]) for k in range(args.steps)) / args.steps * 1e3
-        fl, by = kernel_work(nf, nc, D, B, a.params.numel(), plan)
-        for on, (old, new) in ((plan["folded_bn0_backward"], ("k_bwd_mid", "k_bwd_mid_fold")),
-                               (plan["top_pair"], ("k_top", "k_top_pair"))):
-            if on:  # report the kernel that ran under its own name
-                for d_ in (per, fl, by):
-                    d_[new] = d_.pop(old)
-        dom = max(per, key=per.get)
-        t_s = per[dom] * 1e-6
-        tf = fl[dom] / t_s / 1e12
-        gbs = by[dom] / t_s / 1e9
-        # a kernel with GEMM work is priced on the MFMA roofline (its reference
-        # FLOPs), the gradient reduce on HBM; the other figure rides along
-        if fl[dom] > 0:
-            roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(tf / PEAK_FP32_TFLOPS, 4), "algorithmic_per_launch": fl[dom],
-                    "hbm_gbs_secondary": round(gbs, 1), "hbm_frac_secondary": round(gbs / PEAK_HBM_GBS, 4)}
-        else:
-            roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_per_launch": by[dom]}
-        roof["kernel"] = dom
-        roof["avg_us"] = round(per[dom], 3)
-        roof["traffic"] = load_pmc_traffic(dom)
-        result["roofline"] = roof
-        # the whole step against the same peaks: reference FLOPs per pair x B
-        # over the timed ms_per_step, and the PMC bytes of all the step's
-        # kernels against SURVEY 8d's compulsory bytes per pair
-        fpp = flops_per_pair(nf, nc, D)
-        cbp = compulsory_bytes_per_pair(nf, nc, a.params.numel(), B)
-        step_s = elapsed / args.steps
-        pmc_step = pmc_bytes_per_step(list(per))
-        result["step_roofline"] = {
-            "flops_per_pair": fpp, "flops_per_step": fpp * B,
-            "achieved_tflops": round(fpp * B / step_s / 1e12, 2), "peak_tflops": PEAK_FP32_TFLOPS,
-            "frac_mfma": round(fpp * B / step_s / 1e12 / PEAK_FP32_TFLOPS, 4),
-            "compulsory_bytes_per_pair": round(cbp, 1), "compulsory_bytes_per_step": round(cbp * B),
-            "compulsory_gbs": round(cbp * B / step_s / 1e9, 1),
-            "pmc_bytes_per_step": pmc_step,
-            "pmc_over_compulsory": round(pmc_step / (cbp * B), 2) if pmc_step else None}
-        result["kernel_us"] = {k: round(v, 3) for k, v in per.items()}
-        result["step_plan"] = plan
-        result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)
-        if rank == 0:
-            result["cosine_roofline"] = cosine_roofline(dev, D=D)
-        if world == 1 and not args.no_side_config:  # the other single-GPU BASELINE config (cfg 2)
-            others = [c for c in CONFIGS if c != args.config]
-            result["other_configs"] = {c: side_config_leg(dev, c) for c in others}
-        # drop the training state before the 40 GB (N=1) similarity workspace
-        del tr, model, data, rows
-        graph = None
-        torch.cuda.empty_cache()
-        if not args.no_contrastive:
-            result["contrastive"] = contrastive_leg(dev, pg, world, rank,
-                                                    cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
+    # the training state travels in a dict that run_extras empties before the
+    # 40 GB (N = 1) similarity workspace of the contrastive leg
+    held = {"tr": tr, "model": model, "data": data, "rows": rows}
+    del tr, model, data, rows, step_fn
+    graph = graph_rem = None
+    try:
+        if not args.no_extras:
+            run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, nf, nc, D)
+    except Exception as e:  # the headline is measured: report it whatever an extra leg does
+        print(f"bench: extra legs failed: {e!r}", file=sys.stderr)
+        result["extras_error"] = repr(e)[:300]
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(nf, nc, D, B)
@@ -673,6 +604,94 @@ def main():
         emit(json.dumps(result))
     if pg is not None:
         dist.destroy_process_group()
+
+
+def run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, nf, nc, D):
+    """Per-kernel events and rooflines, the cosine kernel, the side config and
+    the contrastive leg (after the headline measurement)."""
+    from ceo_firm_matching import _native as N
+    tr, rows = held["tr"], held["rows"]
+    # ---- per-kernel HIP events on the launch stream (separate pass, K steps)
+    st = N.stream_ptr(dev)
+    # 2 events per kernel, stamped by the kernel's own dispatch
+    # (tt_train_step_ev -> hipExtLaunchKernelGGL): kernel-only durations
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(12)] for _ in range(args.steps)]
+    for row in evs:
+        for e in row:
+            e.record()  # materialise the hipEvent
+    torch.cuda.synchronize()
+    a = tr.arena
+    for k in range(args.steps):
+        arr = (ctypes.c_void_p * 12)(*[e.cuda_event for e in evs[k]])
+        batch = tr._batch(rows, 0, B, cycle=n_batches)
+        rc = tr.lib.tt_train_step_ev(tr.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
+                                     batch, tr.hp, tr.seed, tr.state.data_ptr(), tr.ws.data_ptr(),
+                                     tr.ws_bytes, tr.grad.data_ptr(), tr.exp_avg.data_ptr(),
+                                     tr.exp_avg_sq.data_ptr(), int(pg is None), st, arr)
+        N.check(rc, "tt_train_step_ev")
+        if pg is not None:
+            tr.allreduce_and_adam()
+    torch.cuda.synchronize()
+    plan = N.step_plan(tr.desc, B)
+    per = {}
+    for i, name in enumerate(KERNELS):
+        if name == "k_bwd_first" and plan["folded_bn0_backward"]:
+            continue  # not launched: its work runs inside k_bwd_mid (folded BN0 backward)
+        per[name] = sum(evs[k][2 * i].elapsed_time(evs[k][2 * i + 1]) for k in range(args.steps)) / args.steps * 1e3
+    fl, by = kernel_work(nf, nc, D, B, a.params.numel(), plan)
+    for on, (old, new) in ((plan["folded_bn0_backward"], ("k_bwd_mid", "k_bwd_mid_fold")),
+                           (plan["top_pair"], ("k_top", "k_top_pair"))):
+        if on:  # report the kernel that ran under its own name
+            for d_ in (per, fl, by):
+                d_[new] = d_.pop(old)
+    dom = max(per, key=per.get)
+    t_s = per[dom] * 1e-6
+    tf = fl[dom] / t_s / 1e12
+    gbs = by[dom] / t_s / 1e9
+    # a kernel with GEMM work is priced on the MFMA roofline (its reference
+    # FLOPs), the gradient reduce on HBM; the other figure rides along
+    if fl[dom] > 0:
+        roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / PEAK_FP32_TFLOPS, 4), "algorithmic_per_launch": fl[dom],
+                "hbm_gbs_secondary": round(gbs, 1), "hbm_frac_secondary": round(gbs / PEAK_HBM_GBS, 4)}
+    else:
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_per_launch": by[dom]}
+    roof["kernel"] = dom
+    roof["avg_us"] = round(per[dom], 3)
+    roof["traffic"] = load_pmc_traffic(dom)
+    result["roofline"] = roof
+    # the whole step against the same peaks: reference FLOPs per pair x B
+    # over the timed ms_per_step, and the PMC bytes of all the step's
+    # kernels against SURVEY 8d's compulsory bytes per pair
+    fpp = flops_per_pair(nf, nc, D)
+    cbp = compulsory_bytes_per_pair(nf, nc, a.params.numel(), B)
+    step_s = elapsed / args.steps
+    pmc_step = pmc_bytes_per_step(list(per))
+    result["step_roofline"] = {
+        "flops_per_pair": fpp, "flops_per_step": fpp * B,
+        "achieved_tflops": round(fpp * B / step_s / 1e12, 2), "peak_tflops": PEAK_FP32_TFLOPS,
+        "frac_mfma": round(fpp * B / step_s / 1e12 / PEAK_FP32_TFLOPS, 4),
+        "compulsory_bytes_per_pair": round(cbp, 1), "compulsory_bytes_per_step": round(cbp * B),
+        "compulsory_gbs": round(cbp * B / step_s / 1e9, 1),
+        "pmc_bytes_per_step": pmc_step,
+        "pmc_over_compulsory": round(pmc_step / (cbp * B), 2) if pmc_step else None}
+    result["kernel_us"] = {k: round(v, 3) for k, v in per.items()}
+    result["step_plan"] = plan
+    result["step_us_sum_of_kernels"] = round(sum(per.values()), 2)
+    if rank == 0:
+        result["cosine_roofline"] = cosine_roofline(dev, D=D)
+    if world == 1 and not args.no_side_config:  # the other single-GPU BASELINE config (cfg 2)
+        others = [c for c in CONFIGS if c != args.config]
+        result["other_configs"] = {c: side_config_leg(dev, c) for c in others}
+    # drop the training state before the 40 GB (N=1) similarity workspace
+    del tr, rows
+    held.clear()
+    gc.collect()
+    torch.cuda.empty_cache()
+    if not args.no_contrastive:
+        result["contrastive"] = contrastive_leg(dev, pg, world, rank,
+                                                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
 
 
 if __name__ == "__main__":

@@ -120,6 +120,42 @@ __device__ __forceinline__ void rep_sum(const float* rep, int stride, float* scr
   __syncthreads();
 }
 
+// rep_sum split in two (issue / finish) so the replica loads can be issued
+// ahead of a kernel's tile loads: vmcnt retires in issue order, so the sum
+// (and the BN-coefficient chain behind it) then waits for the replicas only,
+// not for every tile load issued before them.
+template <int NTH, int N>
+struct RepSum1 {
+  static constexpr int G0 = NTH / N;
+  static constexpr int G = G0 < NREP ? G0 : NREP;
+  static constexpr int PER = NREP / G;
+  static_assert(NTH % N == 0 && NREP % G == 0, "replica groups");
+  float v[PER];
+  __device__ __forceinline__ void issue(const float* rep, int stride) {
+    // groups beyond G re-read group G - 1 (ignored by finish): no branch join
+    const int c = (int)threadIdx.x % N, grp = min((int)threadIdx.x / N, G - 1);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = rep[(grp + k * G) * stride + c];
+  }
+  __device__ __forceinline__ void finish(float* scratch, float* dst) {
+    const int c = (int)threadIdx.x % N, grp = (int)threadIdx.x / N;
+    if (grp < G) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) sum += v[k];
+      scratch[grp * N + c] = sum;
+    }
+    __syncthreads();
+    if (threadIdx.x < N) {
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < G; ++q) sum += scratch[q * N + threadIdx.x];
+      dst[threadIdx.x] = sum;
+    }
+    __syncthreads();
+  }
+};
+
 // rep_sum of two equally shaped replica sets at once (one load round trip),
 // split in two so the caller can work while the loads are in flight:
 //   RepSum2<NTH, N> rs; rs.issue(rep0, rep1, stride);  ...  rs.finish(scratch, dst);
@@ -535,11 +571,12 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   float* rst = smem + L::f_rst;                      // [2*64] BN0 moment sums S1|S2
   TT_STAMP(1, 0);
 
-  // ---- issue every load of the phase first (Z0 rows are padded: no clamp)
-  // this lane's A-operand slices of Z0: row 16w + r, columns 8g.. and 32 + 8g..
-  const float* zr = T.Z0 + (r0 + 16 * w + r) * H0 + 8 * g;
-  const float4 za0 = *reinterpret_cast<const float4*>(zr), za1 = *reinterpret_cast<const float4*>(zr + 4);
-  const float4 zb0 = *reinterpret_cast<const float4*>(zr + 32), zb1 = *reinterpret_cast<const float4*>(zr + 36);
+  // ---- issue every load of the phase first (Z0 rows are padded: no clamp):
+  // the BN0 moment replicas first (their sum and the coefficient chain wait
+  // for them alone), then this lane's A-operand slices of Z0: row 16w + r,
+  // columns 8g.. and 32 + 8g..
+  RepSum1<NTH, 2 * H0> rs;
+  rs.issue(T.st0, 2 * H0);
   float bias[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias[j] = T.b4[16 * j + r];
@@ -551,19 +588,18 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   const int we0 = (int)threadIdx.x, we1 = (int)threadIdx.x + NTH;  // two float4 per thread (named: no array)
   const float4 w4a = *reinterpret_cast<const float4*>(T.W4 + (we0 >> 4) * H0 + 4 * (we0 & 15));
   const float4 w4b = *reinterpret_cast<const float4*>(T.W4 + (we1 >> 4) * H0 + 4 * (we1 & 15));
-  float bn_sh = 0.f, bn_rm = 0.f, bn_rv = 0.f, bn_g = 0.f, bn_be = 0.f;
-  if (w == 0) {
-    const float* rmp = T.rm0 ? T.rm0 : T.g0;  // running stats NULL without buffers (never read then)
-    const float* rvp = T.rv0 ? T.rv0 : T.g0;
-    bn_sh = T.shift0[l];
-    bn_rm = rmp[l];
-    bn_rv = rvp[l];
-    bn_g = T.g0[l];
-    bn_be = T.be0[l];
-  }
+  // (every wave loads them -- wave 0 uses them: a load under a branch would
+  // make hipcc drain vmcnt at the join, i.e. wait for the whole phase here)
+  const float* rmp = T.rm0 ? T.rm0 : T.g0;  // running stats NULL without buffers (never read then)
+  const float* rvp = T.rv0 ? T.rv0 : T.g0;
+  const float bn_sh = T.shift0[l], bn_rm = rmp[l], bn_rv = rvp[l], bn_g = T.g0[l], bn_be = T.be0[l];
+  // the Z0 tile last: needed only after the phase's barrier
+  const float* zr = T.Z0 + (r0 + 16 * w + r) * H0 + 8 * g;
+  const float4 za0 = *reinterpret_cast<const float4*>(zr), za1 = *reinterpret_cast<const float4*>(zr + 4);
+  const float4 zb0 = *reinterpret_cast<const float4*>(zr + 32), zb1 = *reinterpret_cast<const float4*>(zr + 36);
   const bool drop = a.train && a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
-  if (a.train) rep_sum<NTH, 2 * H0>(T.st0, 2 * H0, rsc, rst);
+  if (a.train) rs.finish(rsc, rst);
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
     float mean, inv;

@@ -410,6 +410,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
+    ap.add_argument("--launch", choices=("graph", "steps"), default=os.environ.get("CEO_BENCH_LAUNCH", "graph"),
+                    help="single GPU: hipGraph replay of captured steps, or all K steps issued by one "
+                         "tt_train_steps call (C++ launch loop, no graph)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / cosine legs")
     ap.add_argument("--no-contrastive", action="store_true", help="skip the cfg-5 contrastive leg")
@@ -464,7 +467,9 @@ def main():
     # hipGraph replay of whole steps at every world size: the RCCL all-reduce
     # of the data-parallel step is captured with the kernels (no host work
     # per step); --no-graph launches every step eagerly.
-    use_graph = not args.no_graph and (pg is None or dist.get_backend(pg) == "nccl" or tr.peer is not None)
+    c_steps = args.launch == "steps" and pg is None and not args.no_graph
+    use_graph = not args.no_graph and not c_steps and (pg is None or dist.get_backend(pg) == "nccl" or
+                                                       tr.peer is not None)
     step_fn = lambda: tr.step_cycle(rows, B, n_batches)  # noqa: E731
     for _ in range(args.warmup):
         step_fn()
@@ -526,6 +531,8 @@ def main():
             graph.replay()
         if graph_rem is not None:
             graph_rem.replay()
+    elif c_steps:  # exactly K steps launched by one tt_train_steps call
+        tr.step_cycle_n(rows, B, n_batches, args.steps)
     else:
         for _ in range(args.steps):
             step_fn()
@@ -579,6 +586,7 @@ def main():
                                f"bs={B}/GPU, dropout 0.1, Adam lr 4e-4",
                    "global_batch": B * world, "parallelism": f"dp{world}" if pg is not None else "single",
                    "graph": bool(graph is not None), "graph_chunk": chunk,
+                   "launch": "tt_train_steps" if c_steps else ("hipgraph" if graph is not None else "eager"),
                    "grad_exchange": ("peer-memory one-shot inside k_reduce_adam (+ Adam)" if tr.fused_exchange
                                      else "peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
                                      else ("rccl all-reduce" if pg is not None and dist.get_backend(pg) == "nccl"

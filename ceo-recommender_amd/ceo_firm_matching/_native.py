@@ -31,7 +31,7 @@ _PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("CEO_TT_LIB") or os.path.join(_PKG_PARENT, "lib", "libceo_tt.so")
 EXPORTED = ("tt_abi_version", "tt_param_count", "tt_param_offsets", "tt_buffer_count",
             "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_backward_ex", "tt_embed_forward",
-            "tt_embed_backward", "tt_embed_backward_ex", "tt_train_step", "tt_train_step_ev", "tt_train_step_dp",
+            "tt_embed_backward", "tt_embed_backward_ex", "tt_train_step", "tt_train_steps", "tt_train_step_ev", "tt_train_step_dp",
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
             "tt_nce_workspace_bytes", "tt_nce_norms", "tt_nce_forward", "tt_nce_loss", "tt_nce_backward",
             "tt_rank_workspace_bytes", "tt_retrieval_ranks", "tt_step_plan",
@@ -106,6 +106,7 @@ def lib() -> ctypes.CDLL:
         "tt_backward_ex": (I32, [D, P, P, Bt, P, I32, U64, I64, P, I64, P, P, P, P]),
         "tt_embed_backward_ex": (I32, [D, P, P, Bt, P, I32, U64, I64, P, I64, P, P, P, P]),
         "tt_train_step": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P]),
+        "tt_train_steps": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P]),
         "tt_train_step_ev": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P, ctypes.POINTER(P)]),
         "tt_adam_apply": (I32, [P, P, P, P, I64, H, P, I64, P]),
         "tt_cosine_forward": (I32, [P, P, I64, I32, P, P, P]),

@@ -161,6 +161,26 @@ class FusedTrainer:
             self._check_eager()
         self.steps_host += 1
 
+    def step_cycle_n(self, rows: torch.Tensor, batch_size: int, n_batches: int, n_steps: int, t_base: int = 0):
+        """n_steps graph-free cycle-mode steps in ONE library call
+        (tt_train_steps: the launches are issued from C++, no host work per
+        step); the same steps as n_steps calls of step_cycle.  Data-parallel
+        trainers loop over step_cycle."""
+        if self.dp:
+            for _ in range(n_steps):
+                self.step_cycle(rows, batch_size, n_batches, t_base)
+            return
+        batch = self._batch(rows, 0, batch_size, cycle=n_batches, t_base=t_base)
+        self.ensure_batch(batch_size)
+        N.set_deterministic(self.desc, self.is_deterministic())
+        a = self.arena
+        rc = self.lib.tt_train_steps(self.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
+                                     batch, self.hp, self.seed, self.state.data_ptr(), self.ws.data_ptr(),
+                                     self.ws_bytes, self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                                     self.exp_avg_sq.data_ptr(), int(n_steps), N.stream_ptr(self.device))
+        N.check(rc, "tt_train_steps", batch_size, 64)
+        self.steps_host += n_steps
+
     def allreduce_and_adam(self):
         a = self.arena
         if self.peer is not None:  # mean over ranks + Adam, one launch

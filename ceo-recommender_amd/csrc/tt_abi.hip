@@ -917,6 +917,18 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   return launch_check();
 }
 
+int32_t tt_train_steps(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt, const tt_batch* b,
+                       const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws, int64_t ws_bytes, float* grad,
+                       float* exp_avg, float* exp_avg_sq, int32_t n_steps, tt_stream_t stream) {
+  if (!b || b->cycle <= 0 || n_steps < 0) return TT_ERR_ARG;  // the batch must follow the device step counter
+  for (int32_t k = 0; k < n_steps; ++k) {
+    const int32_t rc = train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg,
+                                       exp_avg_sq, 1, stream, nullptr);
+    if (rc) return rc;
+  }
+  return TT_OK;
+}
+
 int32_t tt_train_step(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt, const tt_batch* b,
                       const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws, int64_t ws_bytes, float* grad,
                       float* exp_avg, float* exp_avg_sq, int32_t apply_adam, tt_stream_t stream) {

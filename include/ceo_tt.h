@@ -196,6 +196,16 @@ int32_t tt_train_step(const tt_model_desc* d, float* params, float* buffers, int
                       void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
                       int32_t apply_adam, tt_stream_t stream);
 
+/* n_steps consecutive tt_train_step launches in one call (cycle-mode
+ * batches: b->cycle > 0, each step's batch taken from the device step
+ * counter, so the arguments do not change between steps): the epoch loop of
+ * training.py:36-57 without a host round trip per step.  Same semantics as
+ * n_steps calls of tt_train_step; returns the first error.                  */
+int32_t tt_train_steps(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
+                       const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state,
+                       void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
+                       int32_t n_steps, tt_stream_t stream);
+
 /* tt_train_step with per-kernel timing: when events != NULL, kernel k of the
  * step (k = 0..5: l0_fwd, l4_fwd, top, bwd_mid, bwd_first, reduce_adam) is
  * launched with hipExtLaunchKernelGGL(..., events[2k], events[2k+1]) (two

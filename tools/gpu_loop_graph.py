@@ -8,7 +8,7 @@ import test_gpu_parity as T
 fails = 0
 for i in range(n):
     try:
-        T.test_graph_replay_matches_eager()
+        T.test_graph_replay_matches_eager(False)  # atomic mode: the optimizer-scale bound
         print(f"{root} run {i}: ok", flush=True)
     except AssertionError as e:
         fails += 1

@@ -479,11 +479,13 @@ def main():
     # 25 / 40 add 0.3-1.1 us), the remainder of K in a second, shorter graph
     graph, graph_rem, chunk = None, None, 1
     if use_graph:
-        # (K <= 32, e.g. the driver's K = 20: all K steps in one graph, one
-        # launch in the timed region -- measured 56.6 vs 57.1 us per step for
-        # 16 + 4 at K = 20, 53.3 us at K = 400)
+        # K split into equal graphs of at most 16 steps (the driver's K = 20:
+        # two of 10 -- four interleaved rounds: 56.0-56.4 us per step against
+        # 56.5-57.1 for one graph of 20 and 57.1 for 16 + 4; graphs of 4-5
+        # steps 56.8-57.5)
         cmax = int(os.environ.get("CEO_BENCH_CHUNK_MAX", "16"))
-        chunk = args.steps if args.steps <= 32 and "CEO_BENCH_CHUNK_MAX" not in os.environ else min(cmax, args.steps)
+        n_graphs = -(-args.steps // cmax)
+        chunk = -(-args.steps // n_graphs)
         rem = args.steps % chunk
         ok = 1
         try:

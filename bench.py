@@ -2,6 +2,12 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2]
 
+``--gpus N`` with N > 1 runs N ranks: under ``torch.distributed.run`` (the
+driver's form) WORLD_SIZE must equal N (else exit 2); started directly, this
+process spawns the N ranks itself (one child per GPU, before any GPU call)
+and exits with their status.  CEO_BENCH_SHARE_GPU=1 puts every rank on GPU 0
+over gloo (a rehearsal on a one-GPU box).
+
 A "step" is one fused training step (forward, weighted MSE, backward, Adam;
 all-reduce of the gradient when N > 1) over one batch of synthetic pairs that
 are already resident in HBM.  Default workload = BASELINE cfg 3 per GPU
@@ -225,24 +231,38 @@ def cosine_roofline(dev, D=128, n=1 << 22, reps=20):
     ms = e0.elapsed_time(e1) / reps
     byts = 4 * (4 * D + 3) * n
     gbs = byts / (ms * 1e-3) / 1e9
-    # measured stream peak on the same box: device copy of a 2 GiB buffer
-    # (read + write bytes / time), the practical HBM ceiling next to the spec
-    src = torch.empty(1 << 29, device=dev)
+    # measured stream ceiling on the same box: the extension's 16-B vector
+    # copy (tt_stream_copy) over a 2 GiB buffer, read + write bytes / time --
+    # the practical HBM rate next to the spec (torch's copy_ is a blit that
+    # runs below it)
+    src = torch.ones(1 << 29, device=dev)
     dst = torch.empty_like(src)
-    for _ in range(2):
-        dst.copy_(src)
+    nbytes = src.numel() * 4
+
+    def copy():
+        N.check(L.tt_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, st), "tt_stream_copy")
+    for _ in range(3):
+        copy()
     torch.cuda.synchronize()
+    e0.record()
+    for _ in range(10):
+        copy()
+    e1.record()
+    torch.cuda.synchronize()
+    stream = 2 * nbytes / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9
+    assert bool((dst[::4096] == 1).all())
     e0.record()
     for _ in range(10):
         dst.copy_(src)
     e1.record()
     torch.cuda.synchronize()
-    stream = 2 * src.numel() * 4 / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9
+    blit = 2 * nbytes / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9
     del src, dst
     return {"kernel": "k_cosine<2,true>", "pairs": n, "D": D, "bytes_per_pair": 4 * (4 * D + 3),
             "avg_us": round(ms * 1e3, 2), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "stream_peak_measured": round(stream, 1),
-            "frac_of_measured_stream": round(gbs / stream, 4),
+            "stream_peak_kernel": "tt_stream_copy (16-B vector loads/stores, 2 GiB)",
+            "frac_of_measured_stream": round(gbs / stream, 4), "torch_copy_gbs": round(blit, 1),
             "achievable_hbm_guide": ACHIEVABLE_HBM_GBS, "frac_of_achievable": round(gbs / ACHIEVABLE_HBM_GBS, 4),
             "pairs_per_s": round(n / (ms * 1e-3), 1)}
 
@@ -402,7 +422,58 @@ def _guard_stdout():
     return emit
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """``--gpus N`` (N > 1) without a launcher: start one child process per
+    GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), as
+    ``torch.distributed.run --nproc-per-node N`` would, and return the exit
+    status (the first failing child's, 0 when all succeed).  Called before
+    anything touches the GPU: this process only waits.  Rank 0's JSON line
+    reaches stdout through the inherited descriptor."""
+    import subprocess
+    share = bool(os.environ.get("CEO_BENCH_SHARE_GPU"))
+    n_dev = torch.cuda.device_count()  # counts devices without initialising HIP
+    if not share and n_dev < n:
+        print(f"bench: --gpus {n} but {n_dev} GPU(s) visible (CEO_BENCH_SHARE_GPU=1 runs every rank on "
+              f"GPU 0 as a rehearsal)", file=sys.stderr)
+        return 2
+    env = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=os.environ.get("MASTER_PORT") or str(_free_port()))
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=dict(env, RANK=str(r), LOCAL_RANK=str(r))))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in pending:  # a failed rank strands the others in a collective
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    n_req = pre.parse_known_args()[0].gpus
+    if "WORLD_SIZE" not in os.environ and n_req > 1:
+        sys.exit(launch_ranks(n_req))
+    if n_req != int(os.environ.get("WORLD_SIZE", "1")):
+        print(f"bench: --gpus {n_req} does not match WORLD_SIZE={os.environ.get('WORLD_SIZE')}", file=sys.stderr)
+        sys.exit(2)
     emit = _guard_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -435,7 +506,7 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29531")
         # CEO_BENCH_BACKEND=gloo: rehearsal of the N > 1 flow on a one-GPU box
         # (RCCL refuses two ranks on one device); gloo steps run eagerly.
-        backend = os.environ.get("CEO_BENCH_BACKEND", "nccl")
+        backend = os.environ.get("CEO_BENCH_BACKEND", "gloo" if os.environ.get("CEO_BENCH_SHARE_GPU") else "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         else:

@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 
 import torch
 
-TT_ABI_VERSION = 3
+TT_ABI_VERSION = 4
 TT_MAX_CAT = 16
 TT_SLOTS_PER_TOWER = 10
 TT_NUM_OFFSETS = 2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER + 1
@@ -25,11 +25,13 @@ TT_ERR_BATCH_TOO_SMALL = -2
 TT_ERR_UNSUPPORTED = -3
 TT_ERR_WORKSPACE = -4
 TT_FLAG_DETERMINISTIC = 1
+TT_STRUCT_MODEL_DESC, TT_STRUCT_BATCH, TT_STRUCT_ADAM_HP, TT_STRUCT_STATE, TT_STRUCT_AR_PEERS = range(5)
+TT_STATE_BYTES = 32  # tt_state: step_done, step_cur (int64), loss_sum, pad0 (f32), pad1 (int64)
 
 _PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # CEO_TT_LIB: diagnostic override (e.g. the -DTT_STAMPS build); the in-tree library otherwise
 LIB_PATH = os.environ.get("CEO_TT_LIB") or os.path.join(_PKG_PARENT, "lib", "libceo_tt.so")
-EXPORTED = ("tt_abi_version", "tt_param_count", "tt_param_offsets", "tt_buffer_count",
+EXPORTED = ("tt_abi_version", "tt_struct_size", "tt_stream_copy", "tt_param_count", "tt_param_offsets", "tt_buffer_count",
             "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_backward_ex", "tt_embed_forward",
             "tt_embed_backward", "tt_embed_backward_ex", "tt_train_step", "tt_train_steps", "tt_train_step_ev", "tt_train_step_dp",
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
@@ -95,6 +97,8 @@ def lib() -> ctypes.CDLL:
     H = ctypes.POINTER(TTAdamHP)
     sig = {
         "tt_abi_version": (I32, []),
+        "tt_struct_size": (I64, [I32]),
+        "tt_stream_copy": (I32, [P, P, I64, P]),
         "tt_param_count": (I64, [D]),
         "tt_param_offsets": (I32, [D, ctypes.POINTER(ctypes.c_int64)]),
         "tt_buffer_count": (I64, [D]),
@@ -143,6 +147,11 @@ def lib() -> ctypes.CDLL:
     v = L.tt_abi_version()
     if v != TT_ABI_VERSION:
         raise NativeLibraryError(f"{LIB_PATH}: ABI version {v}, expected {TT_ABI_VERSION}")
+    for which, st in ((TT_STRUCT_MODEL_DESC, TTModelDesc), (TT_STRUCT_BATCH, TTBatch), (TT_STRUCT_ADAM_HP, TTAdamHP),
+                      (TT_STRUCT_AR_PEERS, TTArPeers)):
+        if L.tt_struct_size(which) != ctypes.sizeof(st):
+            raise NativeLibraryError(f"{LIB_PATH}: sizeof({st.__name__}) = {ctypes.sizeof(st)} here, "
+                                     f"{L.tt_struct_size(which)} in the library")
     _LIB = L
     return L
 

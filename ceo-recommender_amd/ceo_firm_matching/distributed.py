@@ -31,6 +31,35 @@ def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
     return lo, min(lo + per, n)
 
 
+def rank_epoch_order(n: int, epoch: int, rank: int, world: int, shuffle: bool = True, seed: int = 0,
+                     drop_last: bool = False) -> torch.Tensor:
+    """This rank's sample order for ``epoch``: torch 2.10
+    ``DistributedSampler(dataset of n, num_replicas=world, rank, shuffle,
+    seed, drop_last)`` after ``set_epoch(epoch)`` -- a permutation from
+    ``seed + epoch`` (or 0..n-1), padded by wrapping to a multiple of
+    ``world`` (or cut to one), then every world-th index from ``rank`` --
+    built as one int64 tensor instead of Python lists."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    if drop_last and n % world:
+        per = -(-(n - world) // world)
+    else:
+        per = -(-n // world)
+    total = per * world
+    if shuffle:
+        g = torch.Generator()
+        g.manual_seed(seed + epoch)
+        idx = torch.randperm(n, generator=g)
+    else:
+        idx = torch.arange(n, dtype=torch.int64)
+    if total > n:
+        reps = -(-(total - n) // max(n, 1))
+        idx = torch.cat([idx, idx.repeat(reps)[:total - n]])
+    else:
+        idx = idx[:total]
+    return idx[rank:total:world]
+
+
 def world_of(group=None) -> int:
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 

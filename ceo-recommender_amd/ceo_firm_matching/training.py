@@ -84,6 +84,44 @@ def epoch_order_plan(loader: DataLoader, pin: bool = False) -> Optional[Callable
     return build
 
 
+def dp_epoch_order_plan(loader: DataLoader, epoch: int, rank: int, world: int,
+                        pin: bool = False) -> Callable[[], Tuple[torch.Tensor, List[int]]]:
+    """Data-parallel counterpart of ``epoch_order_plan``: this rank's batch
+    order for ``epoch`` under DistributedSampler semantics
+    (``distributed.rank_epoch_order``: permutation from seed + epoch, padded
+    to ceil(N / world) per rank).  A loader that already holds a
+    ``DistributedSampler`` keeps its shuffle / seed / drop_last (its
+    num_replicas and rank must be this process group's); any other loader is
+    sharded as ``DistributedSampler(dataset)`` would (shuffle as the loader's
+    sampler, seed 0).  Batches of the loader's batch size, the last partial
+    one kept unless the loader drops it.  Consumes the global RNG as
+    ``iter(loader)`` does (the iterator's base seed) so the draws after
+    training match the single-process run's."""
+    from torch.utils.data import RandomSampler
+    from torch.utils.data.distributed import DistributedSampler
+    from .distributed import rank_epoch_order
+    samp = loader.sampler
+    n = len(loader.dataset)
+    if isinstance(samp, DistributedSampler):
+        if (samp.num_replicas, samp.rank) != (world, rank):
+            raise ValueError(f"DistributedSampler(num_replicas={samp.num_replicas}, rank={samp.rank}) in a "
+                             f"process group of {world} (this rank {rank})")
+        shuffle, seed, drop = samp.shuffle, samp.seed, samp.drop_last
+    else:
+        shuffle, seed, drop = isinstance(samp, RandomSampler), 0, False
+    bs = loader.batch_size or 1
+    drop_batch = bool(getattr(loader.batch_sampler, "drop_last", False))
+    torch.empty((), dtype=torch.int64).random_(generator=loader.generator)  # the iterator's base seed
+
+    def build():
+        order = rank_epoch_order(n, epoch, rank, world, shuffle=shuffle, seed=seed, drop_last=drop)
+        m = order.numel()
+        sizes = [bs] * (m // bs) + ([m % bs] if m % bs and not drop_batch else [])
+        order = order[:sum(sizes)]
+        return (order.pin_memory() if pin else order), sizes
+    return build
+
+
 def epoch_order(loader: DataLoader) -> Optional[Tuple[torch.Tensor, List[int]]]:
     """``epoch_order_plan`` built at once: (order, batch sizes) or None."""
     plan = epoch_order_plan(loader)
@@ -102,14 +140,57 @@ def _resident_data(loader: DataLoader) -> Optional[Dict[str, torch.Tensor]]:
     return {k: data[k] for k in DATA_KEYS}
 
 
+def _process_group():
+    """(group, rank, world) of an initialised torch.distributed job with more
+    than one rank, else (None, 0, 1)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.group.WORLD, dist.get_rank(), dist.get_world_size()
+    return None, 0, 1
+
+
+def _select_local_device(config: Config):
+    """One process per GPU: a device without an index resolves to the
+    current one, so make that LOCAL_RANK's (when such a device exists; ranks
+    sharing one GPU in a rehearsal keep theirs)."""
+    import os
+    dev = torch.device(config.DEVICE)
+    local = os.environ.get("LOCAL_RANK")
+    if dev.type == "cuda" and dev.index is None and local is not None:
+        if int(local) < torch.cuda.device_count():
+            torch.cuda.set_device(int(local))
+
+
+def _mean_over_ranks(x: float, pg, device) -> float:
+    import torch.distributed as dist
+    dev = device if dist.get_backend(pg) == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, group=pg)
+    return float(t.item()) / dist.get_world_size(pg)
+
+
 def train_model(train_loader: DataLoader, val_loader: DataLoader,
                 metadata: Dict[str, int], config: Config) -> Optional[CEOFirmMatcher]:
-    """Train the CEOFirmMatcher model (reference training.py:15-64)."""
+    """Train the CEOFirmMatcher model (reference training.py:15-64).
+
+    Under an initialised ``torch.distributed`` job with world size > 1 (one
+    process per GPU, ``torchrun``) this is the reference loop under
+    DistributedDataParallel (BASELINE cfg 4): each rank runs on
+    its LOCAL_RANK device, trains on its DistributedSampler shard of every
+    epoch (``dp_epoch_order_plan``) with local BatchNorm statistics, starts
+    from rank 0's parameters, and averages the gradient over the ranks every
+    step (inside the fused step's reduction, the peer-memory exchange, or an
+    RCCL / gloo all-reduce); rank 0 prints the lines, with the epoch loss
+    averaged over the ranks."""
+    pg, rank, world = _process_group()
+    if pg is not None:
+        _select_local_device(config)
     model = CEOFirmMatcher(metadata, config).to(config.DEVICE)
-    print(f"Starting training on {config.DEVICE} for {config.EPOCHS} epochs...")
+    if rank == 0:
+        print(f"Starting training on {config.DEVICE} for {config.EPOCHS} epochs...")
     if torch.device(config.DEVICE).type == "cuda":
-        return _train_fused(model, train_loader, config)
-    return _train_cpu(model, train_loader, config)
+        return _train_fused(model, train_loader, config, pg)
+    return _train_cpu(model, train_loader, config, pg)
 
 
 train = train_model  # the north-star name
@@ -166,6 +247,14 @@ class _EpochSteps:
                 ctypes.CDLL("libamdhip64.so").hipGetLastError()
             except OSError:
                 pass
+        pg = self.tr.pg
+        if pg is not None:  # data parallel: every rank replays, or none does
+            import torch.distributed as dist
+            dev = self.tr.device if dist.get_backend(pg) == "nccl" else "cpu"
+            ok = torch.tensor([0 if self.eager else 1], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=pg)
+            if int(ok.item()) == 0:
+                self.eager, self.graphs = True, None
 
     def run(self, epoch: int):
         if epoch == 0 or self.eager:
@@ -181,27 +270,49 @@ class _EpochSteps:
         self.tr.steps_host += self.n_full
 
 
-def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> CEOFirmMatcher:
+def _dp_loader(loader: DataLoader, rank: int, world: int) -> DataLoader:
+    """Any map-style loader as its data-parallel shard: the same dataset,
+    batch size and collate behind a DistributedSampler (shuffle as the
+    loader's sampler), unless it already holds one."""
+    from torch.utils.data import RandomSampler
+    from torch.utils.data.distributed import DistributedSampler
+    if isinstance(loader.sampler, DistributedSampler):
+        return loader
+    samp = DistributedSampler(loader.dataset, num_replicas=world, rank=rank,
+                              shuffle=isinstance(loader.sampler, RandomSampler))
+    return DataLoader(loader.dataset, batch_size=loader.batch_size, sampler=samp, collate_fn=loader.collate_fn,
+                      drop_last=loader.drop_last, num_workers=loader.num_workers)
+
+
+def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config, pg=None) -> CEOFirmMatcher:
     dev = model.logit_scale.device
     bs = loader.batch_size or 1
-    trainer = FusedTrainer(model, lr=config.LEARNING_RATE, max_batch=max(bs, 2))
+    rank, world = (0, 1) if pg is None else (pg.rank(), pg.size())
+    trainer = FusedTrainer(model, lr=config.LEARNING_RATE, max_batch=max(bs, 2), process_group=pg)
     data = _resident_data(loader)
     if data is not None:
         trainer.set_data(data)
+    elif pg is not None:
+        loader = _dp_loader(loader, rank, world)
     # the epochs' batch orders: global-RNG draws in epoch order, the
     # permutations built on worker threads a few epochs ahead (torch.randperm
     # of the reference's sampler is sequential: 23 ns per pair, 10x an
     # epoch's fused steps), so the device rarely waits for the host
     pool, ahead, depth = None, [], min(_ORDER_AHEAD, config.EPOCHS)
     pin = torch.cuda.is_available()
-    plan = epoch_order_plan(loader, pin) if data is not None and config.EPOCHS > 0 else None
+
+    def plan_of(epoch):
+        if pg is not None:
+            return dp_epoch_order_plan(loader, epoch, rank, world, pin)
+        return epoch_order_plan(loader, pin)
+    plan = plan_of(0) if data is not None and config.EPOCHS > 0 else None
     nxt = None
     if plan is not None:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=depth)
         ahead.append(pool.submit(plan))
-        for _ in range(1, depth):
-            ahead.append(pool.submit(epoch_order_plan(loader, pin)))
+        for e in range(1, depth):
+            ahead.append(pool.submit(plan_of(e)))
         nxt = ahead.pop(0).result()
     runner = None
     if nxt is not None:
@@ -212,6 +323,8 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> C
         if n_full and sizes0[:n_full] == [bs] * n_full:
             rows_dev = torch.empty(len(nxt[0]), dtype=torch.int64, device=dev)
             runner = _EpochSteps(trainer, rows_dev, bs, n_full, len(sizes0), trainer.steps_done())
+            if pg is not None and not _dp_graphs_ok(trainer):
+                runner.eager = True  # a host collective per step (gloo) cannot be captured
     for epoch in range(config.EPOCHS):
         model.train()
         n_batches = 0
@@ -239,9 +352,11 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> C
             # draw nothing from it); the next one is usually built already
             if pool is not None:
                 if epoch + depth < config.EPOCHS:
-                    ahead.append(pool.submit(epoch_order_plan(loader, pin)))
+                    ahead.append(pool.submit(plan_of(epoch + depth)))
                 nxt = ahead.pop(0).result() if ahead else None
         else:
+            if pg is not None and hasattr(loader.sampler, "set_epoch"):
+                loader.sampler.set_epoch(epoch)
             for batch in loader:
                 batch = {k: v.to(dev) for k, v in batch.items()}
                 trainer.set_data(batch)
@@ -249,7 +364,10 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> C
                 n_batches += 1
         if epoch % 5 == 0:
             avg_loss = trainer.pop_loss_sum() / max(n_batches, 1)
-            print(f"Epoch {epoch}: Avg Train Loss = {avg_loss:.4f}")
+            if pg is not None:
+                avg_loss = _mean_over_ranks(avg_loss, pg, dev)
+            if rank == 0:
+                print(f"Epoch {epoch}: Avg Train Loss = {avg_loss:.4f}")
         else:
             trainer.pop_loss_sum(read=False)
     if pool is not None:
@@ -259,19 +377,53 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> C
     return model
 
 
-def _train_cpu(model: CEOFirmMatcher, loader: DataLoader, config: Config) -> CEOFirmMatcher:
+def _dp_graphs_ok(trainer: FusedTrainer) -> bool:
+    """Data-parallel steps can be captured when their exchange is a kernel
+    (peer memory) or an RCCL collective; a gloo all-reduce is host work."""
+    import torch.distributed as dist
+    return trainer.peer is not None or dist.get_backend(trainer.pg) == "nccl"
+
+
+def _train_cpu(model: CEOFirmMatcher, loader: DataLoader, config: Config, pg=None) -> CEOFirmMatcher:
+    """The reference loop with ATen ops; under a process group the DDP form:
+    rank 0's initial parameters everywhere, the rank's DistributedSampler
+    shard, local BatchNorm statistics, gradients averaged over the ranks
+    (one flat all-reduce) before every Adam step."""
+    from .distributed import average_gradients_, broadcast_state_
+    params = list(model.parameters())
+    if pg is not None:
+        loader = _dp_loader(loader, pg.rank(), pg.size())
+        flat = torch.cat([p.detach().reshape(-1) for p in params])
+        broadcast_state_(flat, None, pg)
+        with torch.no_grad():
+            off = 0
+            for p in params:
+                p.copy_(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
     optimizer = optim.Adam(model.parameters(), lr=config.LEARNING_RATE)
     for epoch in range(config.EPOCHS):
         model.train()
         total_loss = 0.0
+        if pg is not None:
+            loader.sampler.set_epoch(epoch)
         for batch in loader:
             optimizer.zero_grad()
             preds = model(batch['firm_numeric'], batch['firm_cat'], batch['ceo_numeric'], batch['ceo_cat'])
             loss = (batch['weights'] * (preds - batch['target']) ** 2).mean()
             loss.backward()
+            if pg is not None:  # DDP: one flat all-reduce (average) of every gradient
+                g = torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel())
+                               for p in params])
+                average_gradients_(g, pg)
+                off = 0
+                for p in params:
+                    p.grad = g[off:off + p.numel()].view_as(p).clone()
+                    off += p.numel()
             optimizer.step()
             total_loss += loss.item()
         avg_loss = total_loss / len(loader)
-        if epoch % 5 == 0:
+        if pg is not None:
+            avg_loss = _mean_over_ranks(avg_loss, pg, "cpu")
+        if epoch % 5 == 0 and (pg is None or pg.rank() == 0):
             print(f"Epoch {epoch}: Avg Train Loss = {avg_loss:.4f}")
     return model

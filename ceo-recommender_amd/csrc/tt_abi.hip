@@ -655,6 +655,17 @@ extern "C" {
 
 int32_t tt_abi_version(void) { return TT_ABI_VERSION; }
 
+int64_t tt_struct_size(int32_t which) {
+  switch (which) {
+    case TT_STRUCT_MODEL_DESC: return (int64_t)sizeof(tt_model_desc);
+    case TT_STRUCT_BATCH: return (int64_t)sizeof(tt_batch);
+    case TT_STRUCT_ADAM_HP: return (int64_t)sizeof(tt_adam_hp);
+    case TT_STRUCT_STATE: return (int64_t)sizeof(tt_state);
+    case TT_STRUCT_AR_PEERS: return (int64_t)sizeof(tt_ar_peers);
+    default: return -1;
+  }
+}
+
 int64_t tt_param_count(const tt_model_desc* d) {
   if (!desc_ok(d)) return TT_ERR_ARG;
   return make_layout(d).n;
@@ -1031,6 +1042,18 @@ int32_t tt_cosine_mse_fwd_bwd(const float* u, const float* v, const float* targe
                               float* dv, float* loss_sum, float* dls_sum, tt_stream_t stream) {
   return cosine_launch(u, v, target, weight, B, D, logit_scale, inv_batch, score, du, dv, loss_sum, dls_sum, true,
                        (hipStream_t)stream);
+}
+
+int32_t tt_stream_copy(const void* src, void* dst, int64_t bytes, tt_stream_t stream) {
+  if (!src || !dst || bytes < 0 || bytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16) return TT_ERR_ARG;
+  const int64_t n4 = bytes / 16;
+  if (n4 == 0) return TT_OK;
+  // 8 blocks per CU of 256 threads: enough loads in flight to saturate HBM
+  const int64_t want = (n4 + COPY_THREADS * COPY_UNROLL - 1) / (COPY_THREADS * COPY_UNROLL);
+  const int grid = (int)std::min<int64_t>(want, 256 * 8);
+  hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(COPY_THREADS), 0, (hipStream_t)stream,
+                     (const float4*)src, (float4*)dst, n4);
+  return (int32_t)hipGetLastError();
 }
 
 

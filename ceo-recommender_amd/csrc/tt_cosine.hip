@@ -188,4 +188,25 @@ __global__ __launch_bounds__(COS_THREADS) void k_cosine_scalar(const float* __re
 
 
 
+// HBM stream probe (tt_stream_copy): 16-B loads and stores, each thread
+// issues its UNROLL loads before any store, grid-stride over the buffer --
+// the same access shape as k_cosine's row streams, so its rate is the
+// ceiling that kernel is quoted against (bench.py cosine_roofline).
+constexpr int COPY_THREADS = 256;
+constexpr int COPY_UNROLL = 4;
+
+__global__ __launch_bounds__(COPY_THREADS) void k_stream_copy(const float4* __restrict__ src,
+                                                              float4* __restrict__ dst, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * COPY_THREADS;
+  int64_t i = (int64_t)blockIdx.x * COPY_THREADS + threadIdx.x;
+  for (; i + (COPY_UNROLL - 1) * stride < n4; i += COPY_UNROLL * stride) {
+    float4 v[COPY_UNROLL];
+#pragma unroll
+    for (int u = 0; u < COPY_UNROLL; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < COPY_UNROLL; ++u) dst[i + u * stride] = v[u];
+  }
+  for (; i < n4; i += stride) dst[i] = src[i];
+}
+
 }  // namespace tt

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TT_ABI_VERSION 3
+#define TT_ABI_VERSION 4
 #define TT_MAX_CAT 16      /* categorical columns per tower */
 
 /* status codes */
@@ -112,6 +112,17 @@ enum {
  * out[52]      logit_scale.            (-1 for absent tables)            */
 
 int32_t tt_abi_version(void);
+
+/* sizeof of the host descriptors as this library was compiled (ABI v4): a
+ * binding checks its own struct definitions against them before the first
+ * call (a struct a field short makes the library read past the caller's
+ * object).  which = TT_STRUCT_*; -1 for an unknown id.                      */
+#define TT_STRUCT_MODEL_DESC 0
+#define TT_STRUCT_BATCH 1
+#define TT_STRUCT_ADAM_HP 2
+#define TT_STRUCT_STATE 3
+#define TT_STRUCT_AR_PEERS 4
+int64_t tt_struct_size(int32_t which);
 
 /* Flat parameter arena size (floats) and per-parameter offsets. */
 int64_t tt_param_count(const tt_model_desc* d);
@@ -237,6 +248,13 @@ int32_t tt_cosine_mse_fwd_bwd(const float* u, const float* v, const float* targe
                               const float* logit_scale, float inv_batch, float* score,
                               float* du, float* dv, float* loss_sum, float* dls_sum,
                               tt_stream_t stream);
+
+/* Device-to-device copy of `bytes` (a multiple of 16; 16-B aligned pointers)
+ * with 16-B vector loads and stores: the HBM stream ceiling of this box,
+ * measured with the same kind of kernel as the bandwidth-bound paths above
+ * (bench.py's cosine roofline quotes it beside the 8 TB/s spec).  Replaces
+ * nothing in the reference (a measurement probe).                           */
+int32_t tt_stream_copy(const void* src, void* dst, int64_t bytes, tt_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Contrastive scoring (BASELINE cfg 5).

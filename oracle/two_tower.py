@@ -252,11 +252,16 @@ def _bn_backward(dy, zhat, invstd, gamma, train=True):
     return dz, dgamma, dbeta
 
 
-def backward(params, cache, dscore, input_grads: bool = False) -> Dict[str, torch.Tensor]:
+def backward(params, cache, dscore, input_grads: bool = False,
+             relu_masks: Optional[Dict[Tuple[int, int], torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
     """Closed-form gradients of sum(dscore * score) w.r.t. every parameter
     (autograd of model.py:67-89 in the mode the forward ran in).  With
     input_grads, also "firm_numeric" / "ceo_numeric": the gradients w.r.t.
-    the numeric inputs (run_deep_extensions.py:564-590 reads f_num.grad)."""
+    the numeric inputs (run_deep_extensions.py:564-590 reads f_num.grad).
+    ``relu_masks[(tower, layer)]`` (bool [B, H]) replaces ReLU's backward
+    mask ``y > 0`` (ATen threshold_backward: zero gradient at y <= 0) -- for
+    tests that bound the gradient over both branches of elements lying
+    within rounding of the kink."""
     grads = {}
     train = cache.get("train", True)
     s, cos, score = cache["s"], cache["cos"], cache["score"]
@@ -275,7 +280,8 @@ def backward(params, cache, dscore, input_grads: bool = False) -> Dict[str, torc
         for li, (lin, bn) in reversed(list(enumerate((("0", "1"), ("4", "5"))))):
             y, noise = c[f"y{li}"], c[f"noise{li}"]
             dr = da * noise if noise is not None else da
-            dy = dr * (y > 0).to(dr.dtype)
+            pas = relu_masks[(ti, li)] if relu_masks is not None and (ti, li) in relu_masks else (y > 0)
+            dy = dr * pas.to(dr.dtype)
             dz, dg, dbe = _bn_backward(dy, c[f"zhat{li}"], c[f"invstd{li}"],
                                        params[f"{t}_tower.{bn}.weight"], train)
             grads[f"{t}_tower.{bn}.weight"] = dg

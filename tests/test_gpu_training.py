@@ -220,3 +220,30 @@ def test_out_of_range_category_code_raises_index_error():
         (f2 if which == "firm" else c2)[3, 1 if which == "firm" else 0] = bad
         with pytest.raises(IndexError):
             m(fn, f2, cn, c2)
+
+
+def test_train_model_data_parallel_two_ranks_one_gpu():
+    """train_model under a 2-rank process group (the north-star train() entry
+    under torchrun), ranks sharing the test box's GPU: fused steps on each
+    rank's DistributedSampler shard, gradients averaged over the peer-memory
+    exchange, epochs after the first replayed from hipGraphs -- equal to the
+    oracle's DDP loop (tests/test_distributed_train.py) at the trained bar, the
+    same parameters on both ranks, lines printed by rank 0 only."""
+    _need_gpu()
+    from ceo_firm_matching import Config
+    from test_distributed_train import check_against_oracle, oracle_ddp_train, run_ddp_train
+    from test_host_pipeline import cli_data
+    world, epochs, seed = 2, 3, 4321
+    res = run_ddp_train(world, "cuda", epochs, seed)
+    cfg = Config()
+    cfg.DROPOUT_P = 0.0
+    train, _ = cli_data(cfg)
+    P, buf, steps = oracle_ddp_train(train, cfg, world, epochs, seed)
+    for rank, sd, printed, same, n_steps in res:
+        assert isinstance(sd, dict), sd
+        assert same is True, rank
+        assert n_steps == steps, (rank, n_steps, steps)
+        lines = [ln for ln in printed.splitlines() if ln.startswith(("Epoch", "Starting"))]
+        assert len(lines) == (2 if rank == 0 else 0), (rank, lines)
+        if rank == 0:
+            check_against_oracle(sd, P, buf, steps, cfg.LEARNING_RATE)

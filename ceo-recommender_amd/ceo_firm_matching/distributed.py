@@ -277,8 +277,11 @@ class PeerExchange:
         an update computed from the local gradient alone."""
         if self.failed():
             raise RuntimeError("peer gradient exchange: a rank did not publish within the wait bound; "
-                               "parameters were left at their last exchanged values "
-                               "(set CEO_TT_PEER_AR=0 to use the RCCL all-reduce)")
+                               "parameters were left at their last exchanged values on the timed-out "
+                               "slices (a peer that saw every flag may have applied that step: the "
+                               "ranks can differ by one step there). The trainer is stopped; build a "
+                               "new one (it broadcasts rank 0's state) or set CEO_TT_PEER_AR=0 to use "
+                               "the RCCL all-reduce")
 
     def _check(self, group) -> bool:
         g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)

@@ -61,14 +61,17 @@ class FusedTrainer:
         # one-launch gradient exchange + Adam over peer memory when every rank
         # can map it and it beats the collective (else the RCCL all-reduce)
         self.peer = PeerExchange.create(n, process_group, dev) if self.dp else None
-        # exchange inside the step's reduction (None: not tried yet).  Only
-        # with one rank per GPU: a rank spinning in its reduction holds LDS and
-        # wave slots that a co-located rank's forward kernels need, so ranks
-        # sharing a device (rehearsals) keep the two-launch form unless
-        # CEO_TT_FUSED_EX=1 (tests with small kernels)
+        # exchange inside the step's reduction (None: not decided yet; the
+        # first data-parallel step validates it against the two-launch form on
+        # this topology, _validate_fused_exchange).  Only with one rank per
+        # GPU: a rank spinning in its reduction holds LDS and wave slots that a
+        # co-located rank's forward kernels need, so ranks sharing a device
+        # (rehearsals) keep the two-launch form unless CEO_TT_FUSED_EX=1
+        # (tests with small kernels); CEO_TT_FUSED_EX=0 turns it off
         import os
-        self.fused_exchange = None if self.peer is not None and (
-            self.peer.co_ranks == 1 or os.environ.get("CEO_TT_FUSED_EX") == "1") else False
+        fx = os.environ.get("CEO_TT_FUSED_EX")
+        self.fused_exchange = None if self.peer is not None and fx != "0" and (
+            self.peer.co_ranks == 1 or fx == "1") else False
         self.max_batch = 0
         self.ws = None
         self.ensure_batch(max_batch)
@@ -127,7 +130,10 @@ class FusedTrainer:
         when the peer exchange is mapped and the reduction's blocks can all be
         resident (tt_train_step_dp; decided once), else reduce -> exchange
         (peer launch or RCCL all-reduce) -> Adam."""
-        if self.peer is not None and self.fused_exchange is not False:
+        if self.peer is not None and self.fused_exchange is None and not torch.cuda.is_current_stream_capturing():
+            self.ensure_batch(n_rows)
+            self.fused_exchange = self._validate_fused_exchange(batch, n_rows)
+        if self.peer is not None and self.fused_exchange is True:
             self.ensure_batch(n_rows)
             N.set_deterministic(self.desc, self.is_deterministic())
             rc = self.peer.train_step(self, batch)
@@ -138,6 +144,58 @@ class FusedTrainer:
             self.fused_exchange = False
         self._launch(batch, n_rows, False)
         self.allreduce_and_adam()
+
+    def _validate_fused_exchange(self, batch, n_rows) -> bool:
+        """Decide once, on this job's real topology, whether the exchange
+        inside the reduction (tt_train_step_dp) may be used: run the first
+        batch both ways in deterministic mode -- the in-reduction exchange,
+        then reduce -> standalone exchange + Adam (itself checked against the
+        collective by PeerExchange.create) -- from the same saved state, and
+        keep the fused form only if every rank finished both without a
+        timeout and got bitwise the same parameters, Adam moments, BN buffers
+        and gradient.  The state is restored (and the exchange regions reset)
+        afterwards, so the real step runs from where it started."""
+        import torch.distributed as dist
+        a = self.arena
+        live = (a.params, a.buffers, a.nbt, self.grad, self.exp_avg, self.exp_avg_sq, self.state)
+        saved = [t.clone() for t in live]
+
+        def restore():
+            torch.cuda.synchronize(self.device)
+            for dst, src in zip(live, saved):
+                dst.copy_(src)
+            self.ws.zero_()  # a timed-out launch may leave accumulators behind
+            if self.pg is not None:
+                self.peer.reset(self.pg)
+            else:
+                self.peer.err.zero_()
+
+        def result():
+            torch.cuda.synchronize(self.device)
+            return torch.cat([a.params, self.exp_avg, self.exp_avg_sq, a.buffers, self.grad]).clone()
+        prev_det = self.deterministic
+        self.deterministic = True
+        N.set_deterministic(self.desc, True)
+        try:
+            rc = self.peer.train_step(self, batch)
+            ok = rc == N.TT_OK
+            fused = result() if ok else None
+            ok = ok and not self.peer.failed()
+            restore()
+            self._launch(batch, n_rows, False)
+            self.allreduce_and_adam()
+            two = result()
+            ok = ok and not self.peer.failed() and torch.equal(fused, two)
+            restore()
+        finally:
+            self.deterministic = prev_det
+            N.set_deterministic(self.desc, self.is_deterministic())
+        if self.pg is not None:
+            dev = self.device if dist.get_backend(self.pg) == "nccl" else "cpu"
+            flag = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.pg)
+            ok = bool(flag.item())
+        return ok
 
     def step(self, rows: Optional[torch.Tensor], row0: int, n_rows: int):
         """One optimizer step on dataset rows rows[row0:row0+n_rows]."""

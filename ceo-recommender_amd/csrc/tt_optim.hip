@@ -271,7 +271,12 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
     }
   }  // owner
   if constexpr (EX) {
-    if (!reduce_exchange(a.x, t, owner, e, gsum, &xok_s) || !owner) return;
+    const bool xok = reduce_exchange(a.x, t, owner, e, gsum, &xok_s);
+    if (!owner) return;
+    if (!xok) {  // failed exchange: p / m / v / grad untouched, but no stale
+      if (kind == 1) a.gacc[e] = 0.f;  // embedding-gradient sums carried into a later step
+      return;
+    }
   }
   a.grad[e] = gsum;
   if (kind == 1) a.gacc[e] = 0.f;

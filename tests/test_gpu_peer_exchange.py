@@ -357,7 +357,7 @@ def test_exchange_inside_reduction_timeout_leaves_parameters():
     ex.regions = [regs[0], None]
     ex.wait_us = 20_000
     try:
-        tr.peer, tr.dp, tr.world, tr.fused_exchange = ex, True, 2, None
+        tr.peer, tr.dp, tr.world, tr.fused_exchange = ex, True, 2, True  # (no validation: the peer never runs)
         shard = {k: torch.from_numpy(v) for k, v in sub(g, "G2/shard0").items()}
         tr.set_data(shard)
         B = shard["target"].shape[0]
@@ -373,6 +373,78 @@ def test_exchange_inside_reduction_timeout_leaves_parameters():
         torch.cuda.synchronize()
         assert int(ex.err.item()) == err1  # sticky: no new waits
         assert torch.equal(tr.arena.params, p0)
+    finally:
+        torch.cuda.synchronize()
+        L.tt_ar_free(ctypes.c_void_p(regs[1]))
+        ex.close()
+
+
+def test_failed_exchange_leaves_no_stale_embedding_gradients():
+    """tt_train_step_dp whose exchange times out must still clear the
+    step's embedding-gradient accumulators (k_reduce_adam kind 1): a later
+    step on the same workspace (here a single-GPU step after the error is
+    cleared) gets exactly its own embedding gradients, not the failed step's
+    added in.  Embedding geometry (meta_test), p = 0, vs the fp64 oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ctypes
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    from ceo_firm_matching import _native as N
+    from ceo_firm_matching.distributed import PeerExchange
+    from ceo_firm_matching.engine import FusedTrainer
+    from oracle import two_tower as O
+    dev = torch.device("cuda:0")
+    g = load_golden("meta_test")
+    meta = meta_of(g)
+    cfg = Config()
+    cfg.LATENT_DIM = int(g["meta/latent"])
+    cfg.DROPOUT_P = 0.0
+    cfg.DEVICE = dev
+    m = CEOFirmMatcher(meta, cfg)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()})
+    m = m.to(dev)
+    tr = FusedTrainer(m, lr=4e-4, max_batch=256, seed=5)
+    L = N.lib()
+    n = tr.arena.params.numel()
+    nbytes = int(L.tt_ar_region_bytes(n))
+    regs = []
+    for _ in range(2):
+        r = ctypes.c_void_p()
+        h = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)()
+        N.check(L.tt_ar_alloc(nbytes, ctypes.byref(r), h), "tt_ar_alloc")
+        regs.append(r.value)
+    ex = PeerExchange(L, regs, regs[0], 0, 2, n, dev)
+    ex.regions = [regs[0], None]
+    ex.wait_us = 20_000
+    try:
+        batch = {k: torch.from_numpy(v) for k, v in sub(g, "batch").items()}
+        B = batch["target"].shape[0]
+        tr.set_data(batch)
+        tr.peer, tr.dp, tr.world, tr.fused_exchange = ex, True, 2, True
+        with pytest.raises(RuntimeError, match="did not publish"):
+            tr.step(None, 0, B)
+        # clear the error, leave the exchange: the next step is a single-GPU one
+        torch.cuda.synchronize()
+        tr.peer, tr.dp, tr.world, tr.fused_exchange = None, False, 1, False
+        tr.state[0] = 0  # the failed step did not count
+        tr.step(None, 0, B)
+        torch.cuda.synchronize()
+        P = {k: torch.from_numpy(v).double() for k, v in sub(g, "init").items() if k in O.param_names(meta)}
+        buf = {k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items() if k in O.buffer_names()}
+        buf = {k: (v if "num_batches" in k else v.double()) for k, v in buf.items()}
+        score, cache, _ = O.forward(P, buf, batch, train=True)
+        _, dscore = O.weighted_mse(score, batch["target"], batch["weights"])
+        grads = O.backward(P, cache, dscore)
+        base = tr.arena.params.data_ptr()
+        checked = 0
+        for name, prm in m.named_parameters():
+            if "embeddings" not in name:
+                continue
+            off = (prm.data_ptr() - base) // 4
+            got = tr.grad[off:off + prm.numel()].view(prm.shape).cpu().double().numpy()
+            assert normwise(got, grads[name].numpy()) < 1e-5, name
+            checked += 1
+        assert checked == len(meta["firm_cat_counts"]) + len(meta["ceo_cat_counts"])
     finally:
         torch.cuda.synchronize()
         L.tt_ar_free(ctypes.c_void_p(regs[1]))

@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=${1:-r04a}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest -v --timeout 400 --timeout-method thread -m gpu \
-  tests/test_gpu_kinks.py tests/test_integration_doc.py tests/test_bench_launch.py \
+  tests/test_gpu_kinks.py tests/test_integration_doc.py "tests/test_gpu_peer_exchange.py" tests/test_bench_launch.py \
   "tests/test_gpu_training.py::test_train_model_data_parallel_two_ranks_one_gpu" tests/test_gpu_cfg4.py \
   > $OUT/tests.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E "PASS|FAIL|ERROR|passed|failed" $OUT/tests.log | tail -40

@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-4 profile of the current build: per-phase stamps (cfg 3), then the
+# PMC counter passes and the HBM traffic summary
+set -o pipefail
+TAG=${1:-r04b}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+CEO_TT_LIB=ceo-recommender_amd/lib/libceo_tt_stamps.so timeout -k 10 200 python tools/stamps.py cfg3 > $OUT/stamps.txt 2>&1 || { tail $OUT/stamps.txt; exit 1; }
+grep -v amdgpu.ids $OUT/stamps.txt
+bash tools/pmc_profile.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+python tools/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt 2>&1
+python tools/pmc_traffic.py $OUT/pmc $OUT/pmc_traffic.json > $OUT/traffic.log 2>&1 && echo pmc ok
+grep -E "k_(l0|l4|top|bwd|reduce)" $OUT/pmc_summary.txt | cut -c1-400

@@ -3,6 +3,8 @@
 # PMC counter passes and the HBM traffic summary
 set -o pipefail
 TAG=${1:-r04b}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 120 python tools/copyprobe/copy_probe.py > $OUT/copy.txt 2>&1 || { tail $OUT/copy.txt; exit 1; }
+cat $OUT/copy.txt
 CEO_TT_LIB=ceo-recommender_amd/lib/libceo_tt_stamps.so timeout -k 10 200 python tools/stamps.py cfg3 > $OUT/stamps.txt 2>&1 || { tail $OUT/stamps.txt; exit 1; }
 grep -v amdgpu.ids $OUT/stamps.txt
 bash tools/pmc_profile.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }

@@ -197,9 +197,28 @@ train = train_model  # the north-star name
 
 
 # epochs whose batch order is built ahead on worker threads (one thread and
-# one pinned order each: 80 MB at 10M pairs); 6 keeps the 10M-pair epoch's
-# permutation (0.23 s per thread) near the device's 33 ms of steps per epoch
-_ORDER_AHEAD = 6
+# one pinned order each: 80 MB at 10M pairs).  torch.randperm of the
+# reference's sampler is sequential (0.23 s per 10M-pair epoch per thread)
+# against 33 ms of fused steps, so as many threads as the process's CPU share
+# allows (the GPU box gives each GPU 16), keeping two for the launching thread
+_ORDER_AHEAD_MAX = 12
+
+
+def _usable_cpus() -> int:
+    import os
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _order_ahead() -> int:
+    return max(2, min(_ORDER_AHEAD_MAX, _usable_cpus() - 2))
 
 
 class _EpochSteps:
@@ -298,7 +317,7 @@ def _train_fused(model: CEOFirmMatcher, loader: DataLoader, config: Config, pg=N
     # permutations built on worker threads a few epochs ahead (torch.randperm
     # of the reference's sampler is sequential: 23 ns per pair, 10x an
     # epoch's fused steps), so the device rarely waits for the host
-    pool, ahead, depth = None, [], min(_ORDER_AHEAD, config.EPOCHS)
+    pool, ahead, depth = None, [], min(_order_ahead(), config.EPOCHS)
     pin = torch.cuda.is_available()
 
     def plan_of(epoch):

@@ -187,3 +187,48 @@ def test_unscreened_large_batch_vs_kink_bounds(p, det):
             continue
         err = bound_error(sd[n].cpu().double().numpy(), plo[n].numpy(), phi[n].numpy(), plo[n].numpy())
         assert err < TOL, ("param", n, err, len(elems))
+
+
+@pytest.mark.parametrize("det", [False, True], ids=["atomics", "deterministic"])
+def test_every_step_gradient_at_the_fused_parameters(det):
+    """Beyond step 1 the parameter comparisons loosen (Adam turns the fp32
+    noise of ~0 gradient components into +-lr steps), so every step of a
+    4-step cfg-3 run (B = 16384, dropout 0.1, unscreened data) is held to the
+    1e-5 bar on its own: the fused step's gradient against the fp64 oracle's
+    gradient AT THE FUSED PARAMETERS of that step (the oracle re-synced to the
+    kernels' trajectory each step), inside the kink bounds."""
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    from ceo_firm_matching.engine import FusedTrainer
+    from oracle import two_tower as O
+    g = load_golden("cfg3")
+    meta = meta_of(g)
+    B, K, p, seed = 16384, 4, 0.1, 2222
+    data = _draw(meta, K * B, 909)
+    cfg = Config()
+    cfg.LATENT_DIM = int(g["meta/latent"])
+    cfg.DROPOUT_P = p
+    cfg.DEVICE = _dev()
+    m = CEOFirmMatcher(meta, cfg)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()})
+    m = m.to(_dev())
+    tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=seed, deterministic=det)
+    tr.set_data({k: v.to(_dev()) for k, v in data.items()})
+    _, buf = _oracle_state(O, g, meta)
+    names = [n for n, _ in m.named_parameters()]
+    for k in range(K):
+        P = {n: prm.detach().cpu().double().clone() for n, prm in m.named_parameters()}
+        tr.step(None, k * B, B)
+        torch.cuda.synchronize()
+        bk = {n: v[k * B:(k + 1) * B] for n, v in data.items()}
+        masks = {(t, l): torch.from_numpy(O.dropout_keep_mask(seed, k + 1, t, l, B, H, p)).double()
+                 for t in range(2) for l, H in enumerate((64, 32))}
+        score, cache, _ = O.forward(P, buf, bk, train=True, masks=masks, p=p)
+        _, dscore = O.weighted_mse(score, bk["target"], bk["weights"])
+        grads = O.backward(P, cache, dscore)
+        lo, hi = grad_bounds(O, P, cache, dscore, kink_elements(cache, masks))
+        for n in names:
+            if excluded_param(n):
+                continue
+            err = bound_error(_grad_of(m, tr, n), lo[n].numpy(), hi[n].numpy(), grads[n].numpy())
+            assert err < TOL, (k, n, err)
+    assert tr.steps_done() == K

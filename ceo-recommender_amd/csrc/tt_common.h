@@ -39,7 +39,7 @@ __device__ __forceinline__ int rep_of_block() { return (int)(blockIdx.x % NREP);
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); }  // uniform: SGPR, scalar branches
 
 // ---------------------------------------------------------------------------
 // v_mfma_f32_16x16x4_f32, fp32 in / fp32 acc (bitwise an fmaf chain).

@@ -460,8 +460,14 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
       for (int p = 0; p < 3; ++p)
         wf[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * j + r) * LDK + 32 * kk + 8 * g);
       mfma_x3(xa, wf, acc[j]);
-      if (j == w) mfma_x3(xs, wf, accs);
     }
+    // the shift row's tile w: its own fragment read (no per-tile branch
+    // between the MFMA chains), the same six-product sequence in every block
+    bf16x8 ws[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      ws[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * w + r) * LDK + 32 * kk + 8 * g);
+    mfma_x3(xs, ws, accs);
   }
   if (a.train) {
     if (g == 0) {
@@ -679,7 +685,16 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
         for (int p = 0; p < 3; ++p)
           wf[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * j + r) * LDK + 32 * kk + 8 * g);
         mfma_x3(xa[kk], wf, acc[j]);
-        if (a.train && j == w) mfma_x3(sa[kk], wf, accs);
+      }
+    }
+    if (a.train && w < 2) {  // the shift row's tile w (one uniform branch, not one per tile)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 ws[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          ws[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * w + r) * LDK + 32 * kk + 8 * g);
+        mfma_x3(sa[kk], ws, accs);
       }
     }
   }
@@ -1890,6 +1905,33 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
   uint32_t rk[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) rk[i] = dropout_row_key(key, r0 + 16 * w + 4 * g + i);
+  // straight-line A0 / Zh0 (bn_relu_drop's arithmetic, bitwise): the four
+  // columns' BN0 coefficients read once, all issued before use; the dropout
+  // keep bits of columns c and c + 32 (j and j + 2) come from one hash
+  // (DROP_HB0 = 5), computed under one uniform branch -- per-element calls
+  // compiled to a branch and an lgkmcnt(0) wait per element
+  float cmu[4], cal[4], cbe[4], cin[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = 16 * j + r;
+    cmu[j] = c0[col];
+    cal[j] = c0[H0 + col];
+    cbe[j] = c0[2 * H0 + col];
+    cin[j] = c0[3 * H0 + col];
+  }
+  const float dscl = drop ? a.drop_scale : 1.f;
+  uint32_t kb = 0xFFFFu;  // bit 4 j + i: element (row i, column 16 j + r) kept
+  if (drop) {
+    kb = 0u;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t h = perm32(rk[i] ^ ((uint32_t)(16 * jp + r) * 0x9E3779B9u));
+        kb |= ((h & 0xFFFFu) >= a.drop_thr ? 1u : 0u) << (4 * jp + i);
+        kb |= ((h >> 16) >= a.drop_thr ? 1u : 0u) << (4 * (jp + 2) + i);
+      }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = 16 * j + r;
@@ -1898,10 +1940,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
       const int64_t row = r0 + 16 * w + 4 * g + i;
       const float z = zz0[j][i];
       const bool ok = row < a.B;
-      const float av = bn_relu_drop(z, c0[col], c0[H0 + col], c0[2 * H0 + col], drop, rk[i], col, a.drop_thr,
-                                    a.drop_scale);
-      a0[j][i] = ok ? av : 0.f;
-      zh0[j][i] = ok ? (z - c0[col]) * c0[3 * H0 + col] : 0.f;
+      float y = (z - cmu[j]) * cal[j] + cbe[j];
+      y = y > 0.f ? y : 0.f;
+      y = ((kb >> (4 * j + i)) & 1u) ? y * dscl : 0.f;  // dscl = 1 without dropout: y * 1 == y
+      a0[j][i] = ok ? y : 0.f;
+      zh0[j][i] = ok ? (z - cmu[j]) * cin[j] : 0.f;
     }
     put_planes4(hs + L::A0i + fold_at(col, 16 * w + 4 * g), L::PL, make_float4(a0[j][0], a0[j][1], a0[j][2], a0[j][3]));
   }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# parity of the new build, A/B bench vs base, stamps + PMC of the new build
+set -o pipefail
+TAG=${1:-r04c}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+bash tools/gpu_ab.sh $TAG 3 "tests/test_gpu_kinks.py tests/test_gpu_parity.py tests/test_gpu_deterministic.py" libceo_tt_base.so libceo_tt_new.so || exit 1
+CEO_TT_LIB=ceo-recommender_amd/lib/libceo_tt_stamps.so timeout -k 10 200 python tools/stamps.py cfg3 > $OUT/stamps.txt 2>&1 || { tail $OUT/stamps.txt; exit 1; }
+grep -v amdgpu.ids $OUT/stamps.txt
+timeout -k 10 120 python tools/copyprobe/copy_probe.py > $OUT/copy.txt 2>&1 || { tail $OUT/copy.txt; exit 1; }
+cat $OUT/copy.txt
+bash tools/pmc_profile.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+python tools/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt 2>&1
+python tools/pmc_traffic.py $OUT/pmc $OUT/pmc_traffic.json > $OUT/traffic.log 2>&1 && echo pmc ok
+grep -E "k_(l0|l4|top|bwd|reduce)" $OUT/pmc_summary.txt | cut -c1-400

@@ -491,6 +491,9 @@ def main():
                     help="skip the other single-GPU config (PMC passes: counters of the headline config only)")
     ap.add_argument("--dp", action="store_true",
                     help="data-parallel step (all-reduce + Adam) even at world size 1 (tests the N>1 path)")
+    ap.add_argument("--no-defer", action="store_true",
+                    help="single GPU: keep the whole gradient reduction in each step's last kernel "
+                         "(default: its late half runs inside the next step's first kernel, TT_FLAG_DEFER_LATE)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -527,7 +530,8 @@ def main():
     cfg.DEVICE = dev
     torch.manual_seed(42)  # identical init on every rank (DDP broadcast semantics)
     model = CEOFirmMatcher(meta, cfg).to(dev)
-    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42, process_group=pg)
+    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42, process_group=pg,
+                      defer_late=(pg is None and not args.no_defer))
     tr.set_data(data)
     n_batches = shard // B
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -609,6 +613,7 @@ def main():
     else:
         for _ in range(args.steps):
             step_fn()
+    tr.flush()  # the last step's deferred late half: inside the timed region (K whole steps)
     torch.cuda.synchronize()
     if pg is not None:
         dist.barrier()
@@ -660,6 +665,8 @@ def main():
                    "global_batch": B * world, "parallelism": f"dp{world}" if pg is not None else "single",
                    "graph": bool(graph is not None), "graph_chunk": chunk,
                    "launch": "tt_train_steps" if c_steps else ("hipgraph" if graph is not None else "eager"),
+                   "late_half": "deferred into the next step's k_l0_fwd" if tr.defer_late and not c_steps
+                                else "in k_reduce_adam",
                    "grad_exchange": ("peer-memory one-shot inside k_reduce_adam (+ Adam)" if tr.fused_exchange
                                      else "peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
                                      else ("rccl all-reduce" if pg is not None and dist.get_backend(pg) == "nccl"
@@ -706,16 +713,28 @@ def run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, 
             e.record()  # materialise the hipEvent
     torch.cuda.synchronize()
     a = tr.arena
+    # the steps as the timed region ran them: with the deferred late half
+    # (TT_FLAG_DEFER_LATE) every step after the first carries the previous
+    # one's late half in its k_l0_fwd, and k_reduce_adam holds the early half
+    tr.flush()
+    defer = tr.defer_late and pg is None
+    batch = None
     for k in range(args.steps):
         arr = (ctypes.c_void_p * 12)(*[e.cuda_event for e in evs[k]])
         batch = tr._batch(rows, 0, B, cycle=n_batches)
+        extra = (N.TT_FLAG_DEFER_LATE | (N.TT_FLAG_LATE_PENDING if k else 0)) if defer else 0
+        tr.desc.flags |= extra
         rc = tr.lib.tt_train_step_ev(tr.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
                                      batch, tr.hp, tr.seed, tr.state.data_ptr(), tr.ws.data_ptr(),
                                      tr.ws_bytes, tr.grad.data_ptr(), tr.exp_avg.data_ptr(),
                                      tr.exp_avg_sq.data_ptr(), int(pg is None), st, arr)
+        tr.desc.flags &= ~extra
         N.check(rc, "tt_train_step_ev")
         if pg is not None:
             tr.allreduce_and_adam()
+    if defer and batch is not None:
+        tr._late_rows, tr._late_batch = B, batch
+        tr.flush()
     torch.cuda.synchronize()
     plan = N.step_plan(tr.desc, B)
     per = {}

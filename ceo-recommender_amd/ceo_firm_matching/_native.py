@@ -25,6 +25,8 @@ TT_ERR_BATCH_TOO_SMALL = -2
 TT_ERR_UNSUPPORTED = -3
 TT_ERR_WORKSPACE = -4
 TT_FLAG_DETERMINISTIC = 1
+TT_FLAG_DEFER_LATE = 2
+TT_FLAG_LATE_PENDING = 4
 TT_STRUCT_MODEL_DESC, TT_STRUCT_BATCH, TT_STRUCT_ADAM_HP, TT_STRUCT_STATE, TT_STRUCT_AR_PEERS = range(5)
 TT_STATE_BYTES = 32  # tt_state: step_done, step_cur (int64), loss_sum, pad0 (f32), pad1 (int64)
 
@@ -33,7 +35,7 @@ _PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("CEO_TT_LIB") or os.path.join(_PKG_PARENT, "lib", "libceo_tt.so")
 EXPORTED = ("tt_abi_version", "tt_struct_size", "tt_stream_copy", "tt_param_count", "tt_param_offsets", "tt_buffer_count",
             "tt_workspace_bytes", "tt_forward", "tt_backward", "tt_backward_ex", "tt_embed_forward",
-            "tt_embed_backward", "tt_embed_backward_ex", "tt_train_step", "tt_train_steps", "tt_train_step_ev", "tt_train_step_dp",
+            "tt_embed_backward", "tt_embed_backward_ex", "tt_train_step", "tt_train_steps", "tt_train_flush", "tt_train_step_ev", "tt_train_step_dp",
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
             "tt_nce_workspace_bytes", "tt_nce_norms", "tt_nce_forward", "tt_nce_loss", "tt_nce_backward",
             "tt_rank_workspace_bytes", "tt_retrieval_ranks", "tt_step_plan",
@@ -111,6 +113,7 @@ def lib() -> ctypes.CDLL:
         "tt_embed_backward_ex": (I32, [D, P, P, Bt, P, I32, U64, I64, P, I64, P, P, P, P]),
         "tt_train_step": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P]),
         "tt_train_steps": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P]),
+        "tt_train_flush": (I32, [D, P, P, P, Bt, H, P, P, I64, P, P, P, P]),
         "tt_train_step_ev": (I32, [D, P, P, P, Bt, H, U64, P, P, I64, P, P, P, I32, P, ctypes.POINTER(P)]),
         "tt_adam_apply": (I32, [P, P, P, P, I64, H, P, I64, P]),
         "tt_cosine_forward": (I32, [P, P, I64, I32, P, P, P]),
@@ -141,7 +144,11 @@ def lib() -> ctypes.CDLL:
         "tt_triplet_backward": (I32, [P, P, I64, I64, I32, I64, I64, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None:
+            if os.environ.get("CEO_TT_LIB"):  # a diagnostic build of an older ABI: bind what it has
+                continue
+            raise NativeLibraryError(f"{LIB_PATH} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     v = L.tt_abi_version()

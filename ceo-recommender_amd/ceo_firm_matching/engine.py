@@ -31,7 +31,7 @@ DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "we
 class FusedTrainer:
     def __init__(self, model: CEOFirmMatcher, lr: float = 4e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_batch: int = 256, seed: Optional[int] = None, process_group=None,
-                 deterministic: Optional[bool] = None):
+                 deterministic: Optional[bool] = None, defer_late: bool = False):
         dev = model.logit_scale.device
         if dev.type != "cuda":
             raise RuntimeError("FusedTrainer needs the model on a HIP device")
@@ -72,6 +72,14 @@ class FusedTrainer:
         fx = os.environ.get("CEO_TT_FUSED_EX")
         self.fused_exchange = None if self.peer is not None and fx != "0" and (
             self.peer.co_ranks == 1 or fx == "1") else False
+        # TT_FLAG_DEFER_LATE: each single-GPU step leaves the late half of its
+        # reduction (W4, BN1 affine, W8, logit_scale, the loss) to the next
+        # step's first kernel; flush() finishes it (run automatically before
+        # the loss, the parameters or a step of another batch size are used)
+        self.defer_late = bool(defer_late)
+        self._late_rows = 0       # batch rows of the step whose late half is pending (0: none)
+        self._late_batch = None   # that step's tt_batch (for tt_train_flush)
+        self._fold_plan = {}
         self.max_batch = 0
         self.ws = None
         self.ensure_batch(max_batch)
@@ -115,15 +123,64 @@ class FusedTrainer:
     def is_deterministic(self) -> bool:
         return self.model.is_deterministic() if self.deterministic is None else bool(self.deterministic)
 
+    def _folded(self, n_rows: int) -> bool:
+        f = self._fold_plan.get(n_rows)
+        if f is None:
+            f = self._fold_plan[n_rows] = N.step_plan(self.desc, n_rows)["folded_bn0_backward"]
+        return f
+
     def _launch(self, batch, n_rows, apply_adam: bool):
         self.ensure_batch(n_rows)
         N.set_deterministic(self.desc, self.is_deterministic())
+        defer_ok = apply_adam and not self.dp and n_rows >= 2 and self._folded(n_rows)
+        pending = False
+        if self._late_rows:
+            if defer_ok and n_rows == self._late_rows:
+                pending = True
+            else:
+                self.flush()
+        defer = self.defer_late and defer_ok
         a = self.arena
-        rc = self.lib.tt_train_step(self.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
-                                    batch, self.hp, self.seed, self.state.data_ptr(), self.ws.data_ptr(),
-                                    self.ws_bytes, self.grad.data_ptr(), self.exp_avg.data_ptr(),
-                                    self.exp_avg_sq.data_ptr(), int(apply_adam), N.stream_ptr(self.device))
+
+        def call(extra):
+            self.desc.flags |= extra
+            try:
+                return self.lib.tt_train_step(self.desc, a.params.data_ptr(), a.buffers.data_ptr(),
+                                              a.nbt.data_ptr(), batch, self.hp, self.seed, self.state.data_ptr(),
+                                              self.ws.data_ptr(), self.ws_bytes, self.grad.data_ptr(),
+                                              self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), int(apply_adam),
+                                              N.stream_ptr(self.device))
+            finally:
+                self.desc.flags &= ~(N.TT_FLAG_DEFER_LATE | N.TT_FLAG_LATE_PENDING)
+        extra = (N.TT_FLAG_DEFER_LATE if defer else 0) | (N.TT_FLAG_LATE_PENDING if pending else 0)
+        rc = call(extra)
+        if rc == N.TT_ERR_UNSUPPORTED and extra:  # geometry without the deferred form: plain step
+            if pending:
+                self.flush()
+            defer = False
+            rc = call(0)
         N.check(rc, "tt_train_step", n_rows, 64)
+        if defer:
+            self._late_rows, self._late_batch = n_rows, batch
+            self.model._pending_flush = self.flush
+        elif self._late_rows:  # (consumed by this step's first kernel)
+            self._late_rows, self._late_batch = 0, None
+            self.model._pending_flush = None
+
+    def flush(self):
+        """Run the pending late half of the last deferred step (tt_train_flush):
+        parameters, Adam moments and the loss sum are then complete."""
+        if not self._late_rows:
+            return
+        N.set_deterministic(self.desc, self.is_deterministic())
+        a = self.arena
+        rc = self.lib.tt_train_flush(self.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
+                                     self._late_batch, self.hp, self.state.data_ptr(), self.ws.data_ptr(),
+                                     self.ws_bytes, self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                                     self.exp_avg_sq.data_ptr(), N.stream_ptr(self.device))
+        N.check(rc, "tt_train_flush")
+        self._late_rows, self._late_batch = 0, None
+        self.model._pending_flush = None
 
     def _launch_dp(self, batch, n_rows):
         """The data-parallel step: the exchange inside the step's reduction
@@ -220,6 +277,7 @@ class FusedTrainer:
         self.steps_host += 1
 
     def step_cycle_n(self, rows: torch.Tensor, batch_size: int, n_batches: int, n_steps: int, t_base: int = 0):
+        # (one C call for all n steps: no deferred late halves between them)
         """n_steps graph-free cycle-mode steps in ONE library call
         (tt_train_steps: the launches are issued from C++, no host work per
         step); the same steps as n_steps calls of step_cycle.  Data-parallel
@@ -230,6 +288,7 @@ class FusedTrainer:
             return
         batch = self._batch(rows, 0, batch_size, cycle=n_batches, t_base=t_base)
         self.ensure_batch(batch_size)
+        self.flush()
         N.set_deterministic(self.desc, self.is_deterministic())
         a = self.arena
         rc = self.lib.tt_train_steps(self.desc, a.params.data_ptr(), a.buffers.data_ptr(), a.nbt.data_ptr(),
@@ -264,6 +323,7 @@ class FusedTrainer:
 
     def pop_loss_sum(self, read: bool = True) -> Optional[float]:
         """Sum of batch-mean losses since the last call (reads => host sync)."""
+        self.flush()  # a deferred late half still has its step's loss to add
         t = self.loss_sum_tensor()
         v = float(t.item()) if read else None
         t.zero_()

@@ -70,6 +70,19 @@ class CEOFirmMatcher(nn.Module):
         # deterministic reductions (TT_FLAG_DETERMINISTIC): None follows
         # torch.use_deterministic_algorithms / CEO_TT_DETERMINISTIC
         self.deterministic: Optional[bool] = None
+        # a FusedTrainer whose last step deferred the late half of its
+        # reduction (TT_FLAG_DEFER_LATE): its flush, run before anything reads
+        # the parameters (forward, tower_embeddings, state_dict)
+        self._pending_flush = None
+
+    def sync_trainer(self):
+        """Finish a deferred optimizer step of the training engine, if any."""
+        if self._pending_flush is not None:
+            self._pending_flush()
+
+    def state_dict(self, *args, **kwargs):
+        self.sync_trainer()
+        return super().state_dict(*args, **kwargs)
 
     def is_deterministic(self) -> bool:
         return N.deterministic_default() if self.deterministic is None else bool(self.deterministic)
@@ -166,6 +179,7 @@ class CEOFirmMatcher(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, f_numeric, f_cat, c_numeric, c_cat):
+        self.sync_trainer()
         if f_numeric.device.type == "cuda":
             return _fused_forward(self, f_numeric, f_cat, c_numeric, c_cat)
         return self._aten_forward(f_numeric, f_cat, c_numeric, c_cat)
@@ -174,6 +188,7 @@ class CEOFirmMatcher(nn.Module):
         """(U, V): the raw firm / CEO tower outputs (model.py:69-77, before the
         L2 normalisation) -- the encoder half that contrastive.py:52-72
         get_embeddings builds on.  One fused autograd node on a HIP device."""
+        self.sync_trainer()
         if f_numeric.device.type == "cuda":
             return _fused_embeddings(self, f_numeric, f_cat, c_numeric, c_cat)
         f = torch.cat([f_numeric] + [e(f_cat[:, i]) for i, e in enumerate(self.firm_embeddings)], dim=1)

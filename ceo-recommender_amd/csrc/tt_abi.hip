@@ -110,6 +110,7 @@ struct WsLayout {
   int64_t Z0[2], Z4[2], dY0[2], dY1[2], st0[2], st1[2], sh0[2], sh1[2], fin0[2], fin1[2], bng[2], lsr;
   int64_t fr, k0s[2], xsh[2];  // folded BN0 backward: replicas (both towers), inv0*gamma0, shift row
   int64_t adam;                // AdamSlot[2]: cached Adam coefficients (k_l0_fwd, k_reduce_adam)
+  int64_t late;                // int64: deferred late half pending (step + 1, 0: none)
   int64_t tgw;
   int64_t slab[2];
   int64_t gacc;
@@ -151,6 +152,7 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
     W.xsh[t] = take(FOLD_MAX_KP);
   }
   W.adam = take(2 * sizeof(AdamSlot) / sizeof(float));
+  W.late = take(2);
   W.gacc = take(L.n);
   const int64_t rows = padded_rows(max_batch);
   W.n_tiles = (int)(rows / ROWS);
@@ -184,10 +186,11 @@ static std::once_flag g_attr_once;
 static void set_lds_attrs() {
   std::call_once(g_attr_once, [] {
     const int mx = (int)LDS_MAX;
-    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true>, (const void*)k_l0_fwd<ROWS, 1, false>,
-                        (const void*)k_l0_fwd<ROWS, 2, true>, (const void*)k_l0_fwd<ROWS, 2, false>,
-                        (const void*)k_l0_fwd<ROWS, 4, true>, (const void*)k_l0_fwd<ROWS, 4, false>,
-                        (const void*)k_l0_fwd<ROWS, 8, true>, (const void*)k_l0_fwd<ROWS, 8, false>,
+    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true, false>, (const void*)k_l0_fwd<ROWS, 1, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 2, true, false>, (const void*)k_l0_fwd<ROWS, 2, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 4, true, false>, (const void*)k_l0_fwd<ROWS, 4, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 8, true, false>, (const void*)k_l0_fwd<ROWS, 8, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 1, true, true>, (const void*)k_l0_fwd<ROWS, 2, true, true>,
                         (const void*)k_l4_fwd<ROWS>,
                         (const void*)k_top<4, 64, false>, (const void*)k_top<8, 64, false>,
                         (const void*)k_top<4, 128, false>, (const void*)k_top<8, 128, false>,
@@ -379,20 +382,30 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.tgw = ws + W.tgw;
   a.det = (d->flags & TT_FLAG_DETERMINISTIC) ? 1 : 0;
   a.xcd_pair = fold ? 1 : 0;  // 64-row tiles on the XCD of the fold kernel's 128-row tile (tile64)
+  a.l0_gx = (int)(padded_rows(b->n_rows) / ROWS);  // k_l0_fwd's row-tile blocks (Plan::n_tiles)
   a.dslot_lsr = ws + W.det_lsr;
 }
 
 // Segments of the parameter arena for k_reduce_adam: W/b ranges come from the
 // per-tile partial slabs (k_top writes n_tiles_top of them, the 64-row
 // kernels n_tiles), BN affine / embeddings / logit_scale from gacc.
+// part: RED_ALL (every range, one k_reduce_adam), RED_EARLY / RED_LATE (the
+// step's reduction split for TT_FLAG_DEFER_LATE: the late half holds W4, the
+// BN1 affine, W8 | b8 and logit_scale -- first read by the NEXT step's
+// k_l4_fwd / k_top -- and zeroes the BN1 moment sums and folds the loss; the
+// early half everything k_l0_fwd of the next step reads).
+enum { RED_ALL = 0, RED_EARLY = 1, RED_LATE = 2 };
 static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout& W, float* ws, const Plan& P,
-                        float* grad) {
+                        float* grad, int part = RED_ALL) {
   RedArgs r;
   std::memset(&r, 0, sizeof(r));
   int k = 0;
+  bool late_range = false;  // set around the late ranges below
+  const int G = part == RED_LATE ? LATE_G : RED_G;
   auto add = [&](int64_t off, int64_t len, int kind, int tower, int64_t so, int n_slabs, float* rep = nullptr,
                  int64_t rep_stride = 0) {
     if (len <= 0) return;
+    if ((part == RED_EARLY && late_range) || (part == RED_LATE && !late_range)) return;
     r.seg[k].off = off;
     r.seg[k].len = len;
     r.seg[k].kind = kind;
@@ -428,13 +441,17 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
       add(s[TT_SLOT_B0], H0, 0, t, L.so[t][1], P.n_tiles);
       add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, bng, BNG);
     }
+    late_range = true;
     add(s[TT_SLOT_W4], s[TT_SLOT_G1] - s[TT_SLOT_W4], 0, t, L.so[t][2], P.n_tiles_mid);
     add(s[TT_SLOT_G1], 2 * H1, 2, t, 0, 0, bng + 2 * H0, BNG);
     // k_top_pair's 64-row partials: more than one round of slab loads, split
-    const int k8 = RED_E == 64 && P.n_tiles_top > RED_G * RED_UNR && P.n_tiles_top <= 2 * RED_G * RED_UNR ? 5 : 0;
+    const int k8 = RED_E == 64 && P.n_tiles_top > G * RED_UNR && P.n_tiles_top <= 2 * G * RED_UNR ? 5 : 0;
     add(s[TT_SLOT_W8], s[TT_SLOT_B8] + d->latent - s[TT_SLOT_W8], k8, t, L.so[t][4], P.n_tiles_top);
+    late_range = false;
   }
+  late_range = true;
   add(L.ls, 1, 2, 0, 0, 0, ws + W.lsr, LSR);
+  late_range = false;
   // element space of k_reduce_adam: every range starts on a block (one
   // segment per block); kind 3 ranges hold every W0 element twice (P and Q
   // halves of one 32-lane group)
@@ -449,9 +466,10 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   // the first replica segment (BN0 affine: no slab loads) fills the next
   // step's Adam-coefficient slot
   r.next_seg = -1;
-  for (int i = 0; i < k && r.next_seg < 0; ++i)
+  for (int i = 0; i < k && r.next_seg < 0 && part != RED_LATE; ++i)
     if (r.seg[i].kind == 2) r.next_seg = i;
-  r.lsr = ws + W.lsr;
+  r.lsr = part == RED_EARLY ? nullptr : ws + W.lsr;  // the loss fold rides with logit_scale's replicas
+  r.late_pending = reinterpret_cast<int64_t*>(ws + W.late);
   r.n_seg = k;
   r.n_slabs = P.n_tiles;
   r.n = L.n;
@@ -462,6 +480,57 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   r.grad = grad;
   return r;
 }
+
+// The per-step fields of a training step's reduction (part as make_red):
+// the BN moment sums it zeroes (BN0's with the early half: k_l0_fwd of the
+// next step accumulates them; BN1's with the late half: k_l4_fwd), the loss
+// target and the Adam hyperparameters.
+template <class A>
+static void red_step_fields(A& r, int part, const WsLayout& W, float* w, int64_t n_rows, tt_state* state,
+                            int32_t apply_adam, float* params, float* exp_avg, float* exp_avg_sq,
+                            const tt_adam_hp* hp, AdamSlot* slots) {
+  r.inv_b = 1.f / (float)n_rows;
+  for (int t = 0; t < 2; ++t) {
+    r.zero_buf[2 * t] = w + W.st0[t];
+    r.zero_len[2 * t] = part == RED_LATE ? 0 : NREP * 2 * H0;
+    r.zero_buf[2 * t + 1] = w + W.st1[t];
+    r.zero_len[2 * t + 1] = part == RED_EARLY ? 0 : NREP * 2 * H1;
+  }
+  r.loss_state = state;
+  if (apply_adam) {
+    r.apply_adam = 1;
+    r.p = params;
+    r.m = exp_avg;
+    r.v = exp_avg_sq;
+    r.lr = hp->lr;
+    r.b1 = hp->beta1;
+    r.b2 = hp->beta2;
+    r.eps = hp->eps;
+    r.adam_slots = slots;
+    r.state = state;
+  }
+}
+
+// A late half in the kernel-argument form (LateRed: MAX_LATE_SEG segments)
+static LateRed to_late(const RedArgs& r) {
+  LateRed q;
+  std::memset(&q, 0, sizeof(q));
+  for (int i = 0; i < r.n_seg; ++i) q.seg[i] = r.seg[i];
+#define TT_CP(f) q.f = r.f;
+  TT_CP(n_seg) TT_CP(n_slabs) TT_CP(n) TT_CP(vn) TT_CP(slab_ld) TT_CP(gacc) TT_CP(grad) TT_CP(lsr) TT_CP(loss_state)
+  TT_CP(apply_adam) TT_CP(p) TT_CP(m) TT_CP(v) TT_CP(lr) TT_CP(b1) TT_CP(b2) TT_CP(eps) TT_CP(adam_slots)
+  TT_CP(next_seg) TT_CP(state) TT_CP(step_host) TT_CP(inv_b) TT_CP(late_pending) TT_CP(late_mark)
+#undef TT_CP
+  for (int i = 0; i < 2; ++i) q.slab[i] = r.slab[i];
+  for (int i = 0; i < 4; ++i) {
+    q.zero_buf[i] = r.zero_buf[i];
+    q.zero_len[i] = r.zero_len[i];
+  }
+  return q;
+}
+// k_l0_fwd blocks per tower row (y) that carry a late half: half of its
+// element blocks each, rounded to 8 so the row tiles keep their XCDs
+static int late_gx(const LateRed& q) { return (int)round_up((q.vn / RED_E + 1) / 2, 8); }
 
 static int launch_check() {
   const hipError_t e = hipGetLastError();
@@ -502,18 +571,34 @@ static void launch(K kern, dim3 g, dim3 b, size_t lds, hipStream_t s, Evs ev, A.
     hipLaunchKernelGGL(kern, g, b, lds, s, args...);
 }
 
-static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
+// k_l0_fwd's instance for this step, or -1 when a deferred late half rides
+// along (late != NULL) and no LATE instance covers the geometry
+static int l0_late_ok(const StepArgs& a) {
+  return a.tw[0].num_vec && a.tw[1].num_vec && l0_ks(std::max(a.tw[0].kp, a.tw[1].kp)) <= 2;
+}
+static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}, const LateRed* late = nullptr) {
   // instance by the widest tower input (32-wide K steps held in registers)
   // and whether both towers take the aligned numeric-only gather
   const int ks = l0_ks(std::max(a.tw[0].kp, a.tw[1].kp));
   const bool vec = a.tw[0].num_vec && a.tw[1].num_vec;
-  const dim3 grid(P.n_tiles, 2), blk(4 * ROWS);
+  const dim3 blk(4 * ROWS);
+  LateRed none;
+  std::memset(&none, 0, sizeof(none));
+  if (late) {  // the caller checked l0_late_ok
+    const dim3 grid(P.n_tiles + late_gx(*late), 2);
+    if (ks == 1)
+      launch(k_l0_fwd<ROWS, 1, true, true>, grid, blk, P.lds_l0, s, ev, a, *late);
+    else
+      launch(k_l0_fwd<ROWS, 2, true, true>, grid, blk, P.lds_l0, s, ev, a, *late);
+    return;
+  }
+  const dim3 grid(P.n_tiles, 2);
 #define TT_L0(KS)                                                                   \
   if (ks == KS) {                                                                   \
     if (vec)                                                                        \
-      launch(k_l0_fwd<ROWS, KS, true>, grid, blk, P.lds_l0, s, ev, a);             \
+      launch(k_l0_fwd<ROWS, KS, true, false>, grid, blk, P.lds_l0, s, ev, a, none); \
     else                                                                            \
-      launch(k_l0_fwd<ROWS, KS, false>, grid, blk, P.lds_l0, s, ev, a);            \
+      launch(k_l0_fwd<ROWS, KS, false, false>, grid, blk, P.lds_l0, s, ev, a, none);\
     return;                                                                         \
   }
   TT_L0(1)
@@ -855,7 +940,12 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
-  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
+  // TT_FLAG_DEFER_LATE / TT_FLAG_LATE_PENDING: single-GPU Adam steps of the
+  // folded plan only (decided here, before anything is enqueued)
+  const bool defer = (d->flags & TT_FLAG_DEFER_LATE) != 0, pending = (d->flags & TT_FLAG_LATE_PENDING) != 0;
+  if ((defer || pending) && (!apply_adam || x || !c.P.fold)) return TT_ERR_UNSUPPORTED;
+  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad, defer ? RED_EARLY : RED_ALL);
+  r.late_mark = defer ? 1 : -1;
   if (x) {
     // every block of the reduction waits for its peers' same block: all of
     // them (co_ranks grids when ranks share this device) must be resident at
@@ -894,7 +984,14 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     }
     return e;
   };
-  launch_l0(a, c.P, s, ev(0));
+  if (pending && !l0_late_ok(a)) return TT_ERR_UNSUPPORTED;
+  LateRed late;
+  if (pending) {  // the previous step's late half (same batch size: the caller flushes otherwise)
+    RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
+    red_step_fields(lr, RED_LATE, c.W, w, b->n_rows, state, 1, params, exp_avg, exp_avg_sq, hp, a.adam_slots);
+    late = to_late(lr);
+  }
+  launch_l0(a, c.P, s, ev(0), pending ? &late : nullptr);
   det_fold(a, c.P, DET_L0, s);
   launch_l4(a, c.P, s, ev(1));
   det_fold(a, c.P, DET_L4, s);
@@ -904,27 +1001,28 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   det_fold(a, c.P, DET_MID, s);
   launch_first(a, c.P, s, ev(4));
   det_fold(a, c.P, DET_FIRST, s);
-  r.inv_b = 1.f / (float)b->n_rows;
-  for (int t = 0; t < 2; ++t) {
-    r.zero_buf[2 * t] = w + c.W.st0[t];
-    r.zero_len[2 * t] = NREP * 2 * H0;
-    r.zero_buf[2 * t + 1] = w + c.W.st1[t];
-    r.zero_len[2 * t + 1] = NREP * 2 * H1;
-  }
-  r.loss_state = state;
-  if (apply_adam) {
-    r.apply_adam = 1;
-    r.p = params;
-    r.m = exp_avg;
-    r.v = exp_avg_sq;
-    r.lr = hp->lr;
-    r.b1 = hp->beta1;
-    r.b2 = hp->beta2;
-    r.eps = hp->eps;
-    r.adam_slots = a.adam_slots;
-    r.state = state;
-  }
+  red_step_fields(r, defer ? RED_EARLY : RED_ALL, c.W, w, b->n_rows, state, apply_adam, params, exp_avg,
+                  exp_avg_sq, hp, a.adam_slots);
   launch_reduce(r, s, ev(5), x != nullptr);
+  return launch_check();
+}
+
+int32_t tt_train_flush(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt, const tt_batch* b,
+                       const tt_adam_hp* hp, tt_state* state, void* ws, int64_t ws_bytes, float* grad,
+                       float* exp_avg, float* exp_avg_sq, tt_stream_t stream) {
+  if (!params || !buffers || !nbt || !state || !ws || !grad || !hp || !exp_avg || !exp_avg_sq) return TT_ERR_ARG;
+  Ctx c;
+  int rc = prepare(d, b, ws_bytes, 2, &c);
+  if (rc) return rc;
+  if (!c.P.fold) return TT_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  float* w = (float*)ws;
+  RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
+  red_step_fields(lr, RED_LATE, c.W, w, b->n_rows, state, 1, params, exp_avg, exp_avg_sq, hp,
+                  reinterpret_cast<AdamSlot*>(w + c.W.adam));
+  const LateRed late = to_late(lr);
+  hipLaunchKernelGGL(k_reduce_late, dim3((unsigned)(late.vn / RED_E)), dim3(RED_E * LATE_G), 0, s, late);
+  hipLaunchKernelGGL(k_clear_late, dim3(1), dim3(1), 0, s, late.late_pending);
   return launch_check();
 }
 

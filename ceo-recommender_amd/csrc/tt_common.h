@@ -453,6 +453,7 @@ struct StepArgs {
   int det;               // deterministic reductions (TT_FLAG_DETERMINISTIC): slots + k_det_fold
   float* dslot_lsr;      // det: per-block (dls, loss) partials [blocks][2]
   int xcd_pair;          // folded step: 64-row kernels take XCD-paired tiles (tile64)
+  int l0_gx;             // k_l0_fwd's row-tile blocks along x (more blocks: a deferred late half)
 };
 
 // Row tile of a 64-row kernel's block (k_l0_fwd, k_l4_fwd, k_top_pair).
@@ -758,8 +759,11 @@ struct RedExchange {
   uint64_t wait_ticks;               // wait bound in s_memrealtime ticks (100 MHz)
 };
 
-struct RedArgs {
-  Seg seg[MAX_SEG];
+// NS: segment capacity (the whole arena: MAX_SEG; a deferred late half,
+// LateRed below: MAX_LATE_SEG -- it rides in k_l0_fwd's kernel arguments)
+template <int NS>
+struct RedArgsN {
+  Seg seg[NS];
   int32_t n_seg;
   int32_t n_slabs;
   int64_t n;
@@ -781,6 +785,17 @@ struct RedArgs {
   int64_t step_host;
   float inv_b;           // 1 / batch rows (kinds 3, 4)
   RedExchange x;         // k_reduce_adam<PRE, true>: mean over ranks before Adam
+  // deferred late half (TT_FLAG_DEFER_LATE): the early half of step t
+  // records t + 1 in *late_pending (0: nothing deferred; a zeroed workspace
+  // holds 0); a late half runs only when *late_pending == state->step_done + 1,
+  // and takes its Adam step from step_done (k_l0_fwd of step t + 1 rewrites
+  // step_cur meanwhile)
+  int64_t* late_pending;
+  int32_t late_mark;     // early half: 1 records t + 1 (deferring), -1 records 0 (not deferring), 0 leaves it
 };
+using RedArgs = RedArgsN<MAX_SEG>;
+constexpr int MAX_LATE_SEG = 8;
+using LateRed = RedArgsN<MAX_LATE_SEG>;
+constexpr int LATE_G = 4;  // slab groups of a late-half block: 64 elements x 4 = k_l0_fwd's 256 threads
 
 }  // namespace tt

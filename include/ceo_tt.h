@@ -66,6 +66,24 @@ typedef struct tt_model_desc {
  *   under torch.manual_seed (training.py:36-57); so is a fused step with
  *   this flag.  The workspace layout does not depend on the flags.       */
 #define TT_FLAG_DETERMINISTIC 1
+/* TT_FLAG_DEFER_LATE (ABI v4): tt_train_step* runs only the EARLY half of the
+ *   step's gradient reduction + Adam (embeddings, W0 / b0, BN0 affine: what
+ *   the next step's first kernel reads); the LATE half (W4 / b4, BN1 affine,
+ *   W8 / b8, logit_scale, and the step's loss into state->loss_sum) stays
+ *   pending on the workspace.  Until it runs those parameters, their Adam
+ *   moments and loss_sum hold the previous step's values.
+ * TT_FLAG_LATE_PENDING: the previous step on this workspace deferred its late
+ *   half (same batch size): run it inside this step's first kernel, as extra
+ *   workgroups beside the row tiles -- the step keeps five launches and the
+ *   late half leaves the critical path.
+ * tt_train_flush runs a pending late half on its own (before parameters,
+ *   moments or the loss are read, or a step of another batch size).  A late
+ *   half runs only if the workspace records one (the step counter makes a
+ *   stale LATE_PENDING a no-op on the device).  Both flags: single-GPU Adam
+ *   steps (apply_adam = 1) of the folded plan (tt_step_plan info[0] = 1);
+ *   otherwise TT_ERR_UNSUPPORTED, nothing enqueued.                         */
+#define TT_FLAG_DEFER_LATE 2
+#define TT_FLAG_LATE_PENDING 4
 
 /* One batch, described over dataset-resident arrays.  Row i of the batch is
  * dataset row rows[row0 + i] (or row0 + i when rows == NULL).  With cycle > 0
@@ -206,6 +224,15 @@ int32_t tt_train_step(const tt_model_desc* d, float* params, float* buffers, int
                       const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state,
                       void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
                       int32_t apply_adam, tt_stream_t stream);
+
+/* The pending late half of the last TT_FLAG_DEFER_LATE step on this
+ * workspace (b: that step's batch; only n_rows and the geometry are used),
+ * then the workspace records none.  A no-op on the device when nothing is
+ * pending.  Replaces the remainder of optim.Adam.step (training.py:55).     */
+int32_t tt_train_flush(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
+                       const tt_batch* b, const tt_adam_hp* hp, tt_state* state, void* ws,
+                       int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
+                       tt_stream_t stream);
 
 /* n_steps consecutive tt_train_step launches in one call (cycle-mode
  * batches: b->cycle > 0, each step's batch taken from the device step

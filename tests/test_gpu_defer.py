@@ -1,0 +1,199 @@
+"""Deferred late half of the gradient reduction (TT_FLAG_DEFER_LATE,
+DESIGN 10): a step's W4 / BN1-affine / W8 / logit_scale reduction + Adam and
+its loss fold run inside the NEXT step's first kernel (or in tt_train_flush),
+so the step keeps five launches and that work leaves the critical path.
+
+* K deferred steps back to back, then the flush: the same training as K
+  plain steps (training.py:44-57) -- parameters, Adam moments, BN buffers
+  and the loss sum (the late half sums its slabs in another fixed order, so
+  at the optimizer-scale bound, as graph-vs-eager in atomic mode), and both
+  against the fp64 oracle's K-step trajectory at the trained bar;
+* graph-replayed deferred steps are bitwise the eager deferred steps
+  (deterministic mode), across the replay boundaries;
+* a stale TT_FLAG_LATE_PENDING (nothing deferred on the workspace) is a
+  no-op on the device: bitwise the plain step;
+* a batch-size change flushes first; reading the model (state_dict, forward)
+  flushes.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import excluded_param, load_golden, meta_of, normwise, sub
+
+pytestmark = pytest.mark.gpu
+B = 16384
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _setup(p=0.1, n_rows=8 * B, seed=5):
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    g = load_golden("cfg3")
+    meta = meta_of(g)
+    cfg = Config()
+    cfg.LATENT_DIM = int(g["meta/latent"])
+    cfg.DROPOUT_P = p
+    cfg.DEVICE = _dev()
+    rng = np.random.default_rng(seed)
+    data = {
+        "firm_numeric": torch.from_numpy(rng.standard_normal((n_rows, meta["n_firm_numeric"])).astype(np.float32)),
+        "firm_cat": torch.zeros(n_rows, 0, dtype=torch.int64),
+        "ceo_numeric": torch.from_numpy(rng.standard_normal((n_rows, meta["n_ceo_numeric"])).astype(np.float32)),
+        "ceo_cat": torch.zeros(n_rows, 0, dtype=torch.int64),
+        "target": torch.from_numpy(rng.standard_normal((n_rows, 1)).astype(np.float32)),
+        "weights": torch.from_numpy(rng.uniform(1, 10, (n_rows, 1)).astype(np.float32)),
+    }
+    init = {k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()}
+
+    def make(defer, det=True):
+        from ceo_firm_matching.engine import FusedTrainer
+        m = CEOFirmMatcher(meta, cfg)
+        m.load_state_dict(init)
+        m = m.to(_dev())
+        tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=77, deterministic=det, defer_late=defer)
+        tr.set_data({k: v.to(_dev()) for k, v in data.items()})
+        return m, tr
+    return g, meta, data, make
+
+
+def _state(m, tr):
+    tr.flush()
+    torch.cuda.synchronize()
+    return np.concatenate([tr.arena.params.cpu().numpy(), tr.exp_avg.cpu().numpy(), tr.exp_avg_sq.cpu().numpy(),
+                           tr.arena.buffers.cpu().numpy()])
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_deferred_steps_equal_plain_steps_and_the_oracle(p):
+    from oracle import two_tower as O
+    g, meta, data, make = _setup(p=p)
+    K = 4
+    out = {}
+    for defer in (False, True):
+        m, tr = make(defer)
+        for k in range(K):
+            tr.step(None, k * B, B)
+        assert tr._late_rows == (B if defer else 0)
+        loss = tr.pop_loss_sum()  # flushes the last late half first
+        assert tr._late_rows == 0 and m._pending_flush is None
+        assert tr.steps_done() == K
+        out[defer] = ({n: q.detach().cpu().double().numpy().copy() for n, q in m.named_parameters()}, loss,
+                      {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items() if "running" in k})
+    (pp, lp, bp), (pd, ld, bd) = out[False], out[True]
+    assert abs(ld - lp) <= 1e-5 * abs(lp), (ld, lp)
+    lr_steps = 4e-4 * K
+    for n in pp:
+        if excluded_param(n):
+            continue
+        ok = normwise(pd[n], pp[n]) < 1e-5 or np.max(np.abs(pd[n] - pp[n])) <= 5e-2 * lr_steps
+        assert ok, (n, normwise(pd[n], pp[n]))
+    for k in bp:
+        if "running_mean" in k:
+            assert np.max(np.abs(bd[k] - bp[k])) <= lr_steps, k
+        else:
+            assert normwise(bd[k], bp[k]) < 1e-5, k
+    # the deferred run against the fp64 oracle's trajectory (its masks: the kernels' hash stream)
+    P = {k: torch.from_numpy(v).double() for k, v in sub(g, "init").items() if k in O.param_names(meta)}
+    buf = {k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items() if k in O.buffer_names()}
+    buf = {k: (v if "num_batches" in k else v.double()) for k, v in buf.items()}
+    opt = O.Adam(P, lr=4e-4)
+    l64 = 0.0
+    for k in range(K):
+        bk = {n: v[k * B:(k + 1) * B] for n, v in data.items()}
+        masks = None
+        if p > 0:
+            masks = {(t, l): torch.from_numpy(O.dropout_keep_mask(77, k + 1, t, l, B, H, p)).double()
+                     for t in range(2) for l, H in enumerate((64, 32))}
+        loss, _, buf = O.train_step(P, buf, opt, bk, masks=masks, p=p)
+        l64 += float(loss)
+    assert abs(ld - l64) <= 1e-5 * abs(l64), (ld, l64)
+    for n, v in P.items():
+        if excluded_param(n):
+            continue
+        ok = normwise(pd[n], v.numpy()) < 1e-4 or np.max(np.abs(pd[n] - v.numpy())) <= 5e-2 * lr_steps
+        assert ok, (n, normwise(pd[n], v.numpy()))
+
+
+def test_deferred_graph_replay_bitwise_equals_eager():
+    """Cycle-mode deferred steps replayed from two captured 4-step graphs vs
+    the same 8 steps eager: bitwise (deterministic mode), loss included."""
+    _, _, data, make = _setup(p=0.1)
+    rows = torch.randperm(8 * B, device=_dev(), generator=torch.Generator(device=_dev()).manual_seed(3))
+    res = []
+    for use_graph in (False, True):
+        m, tr = make(True)
+        tr.step_cycle(rows, B, 8)  # eager first step: the graphs start with a late half pending
+        if use_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(4):
+                    tr.step_cycle(rows, B, 8)
+            graph.replay()
+            graph.replay()
+        else:
+            for _ in range(8):
+                tr.step_cycle(rows, B, 8)
+        loss = tr.pop_loss_sum()
+        res.append((_state(m, tr), loss, tr.steps_done()))
+    (a, la, na), (b, lb, nb) = res
+    assert na == nb == 9
+    assert la == lb
+    assert np.array_equal(a, b)
+
+
+def test_stale_pending_flag_is_a_noop():
+    """TT_FLAG_LATE_PENDING with nothing deferred on the workspace (a host
+    that lost track) runs no late half: bitwise the plain step."""
+    from ceo_firm_matching import _native as N
+    _, _, _, make = _setup(p=0.1)
+    res = []
+    for stale in (False, True):
+        m, tr = make(False)
+        tr.step(None, 0, B)
+        if stale:  # pretend the previous step deferred: the next step carries a late half
+            tr._late_rows, tr._late_batch = B, tr._batch(None, 0, B)
+        tr.step(None, B, B)
+        assert tr._late_rows == 0
+        res.append((_state(m, tr), tr.pop_loss_sum()))
+    (a, la), (b, lb) = res
+    assert la == lb and np.array_equal(a, b)
+    assert N.lib().tt_train_flush is not None
+
+
+def test_batch_size_change_and_model_reads_flush():
+    from ceo_firm_matching import _native as N
+    _, _, data, make = _setup(p=0.0)
+    sizes = [B, B, 12288, 12288, B]
+    out = []
+    for defer in (False, True):
+        m, tr = make(defer)
+        off = 0
+        for bs in sizes:
+            tr.step(None, off, bs)
+            off += bs
+        if defer:
+            assert tr._late_rows == B and m._pending_flush is not None
+            sd = m.state_dict()  # reading the model finishes the deferred step
+            assert tr._late_rows == 0 and m._pending_flush is None
+            with torch.no_grad():
+                m.eval()
+                s1 = m(data["firm_numeric"][:256].to(_dev()), data["firm_cat"][:256].to(_dev()),
+                       data["ceo_numeric"][:256].to(_dev()), data["ceo_cat"][:256].to(_dev()))
+        else:
+            sd = m.state_dict()
+        out.append(({k: v.detach().cpu().double().numpy().copy() for k, v in sd.items()}, tr.pop_loss_sum()))
+    (a, la), (b, lb) = out
+    assert abs(la - lb) <= 1e-5 * abs(la)
+    for k in a:
+        if excluded_param(k) or "num_batches" in k or "running_mean" in k:
+            continue
+        ok = normwise(b[k], a[k]) < 1e-5 or np.max(np.abs(b[k] - a[k])) <= 5e-2 * 4e-4 * len(sizes)
+        assert ok, (k, normwise(b[k], a[k]))
+    assert N.step_plan(m.tt_desc(), 12288)["folded_bn0_backward"]

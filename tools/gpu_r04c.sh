@@ -1,8 +1,9 @@
 #!/bin/bash
-# parity of the new build, A/B bench vs base, stamps + PMC of the new build
+# parity of the current build (incl. the deferred late half), A/B bench vs
+# earlier builds, stamps + PMC of the current build
 set -o pipefail
 TAG=${1:-r04c}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
-bash tools/gpu_ab.sh $TAG 3 "tests/test_gpu_kinks.py tests/test_gpu_parity.py tests/test_gpu_deterministic.py" libceo_tt_base.so libceo_tt_new.so || exit 1
+bash tools/gpu_ab.sh $TAG 2 "tests/test_gpu_defer.py tests/test_gpu_kinks.py tests/test_gpu_parity.py tests/test_gpu_deterministic.py tests/test_gpu_peer_exchange.py tests/test_gpu_training.py" libceo_tt_base.so@--no-defer libceo_tt_new.so@--no-defer libceo_tt.so@--no-defer libceo_tt.so || exit 1
 CEO_TT_LIB=ceo-recommender_amd/lib/libceo_tt_stamps.so timeout -k 10 200 python tools/stamps.py cfg3 > $OUT/stamps.txt 2>&1 || { tail $OUT/stamps.txt; exit 1; }
 grep -v amdgpu.ids $OUT/stamps.txt
 timeout -k 10 120 python tools/copyprobe/copy_probe.py > $OUT/copy.txt 2>&1 || { tail $OUT/copy.txt; exit 1; }

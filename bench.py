@@ -282,7 +282,7 @@ def side_config_leg(dev, name, steps=200, warmup=20):
     cfg.DEVICE = dev
     torch.manual_seed(42)
     model = CEOFirmMatcher(meta, cfg).to(dev)
-    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42)
+    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42, defer_late=True)
     tr.set_data(data)
     n_batches = n_total // B
     rows = torch.randperm(n_total, device=dev, generator=torch.Generator(device=dev).manual_seed(1000))
@@ -305,6 +305,7 @@ def side_config_leg(dev, name, steps=200, warmup=20):
     t0 = time.perf_counter()
     for _ in range(steps // chunk):
         graph.replay()
+    tr.flush()
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
     n = (steps // chunk) * chunk

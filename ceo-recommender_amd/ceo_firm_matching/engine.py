@@ -79,7 +79,7 @@ class FusedTrainer:
         self.defer_late = bool(defer_late)
         self._late_rows = 0       # batch rows of the step whose late half is pending (0: none)
         self._late_batch = None   # that step's tt_batch (for tt_train_flush)
-        self._fold_plan = {}
+        self._no_defer = set()    # batch sizes whose geometry has no deferred form (TT_ERR_UNSUPPORTED)
         self.max_batch = 0
         self.ws = None
         self.ensure_batch(max_batch)
@@ -123,16 +123,10 @@ class FusedTrainer:
     def is_deterministic(self) -> bool:
         return self.model.is_deterministic() if self.deterministic is None else bool(self.deterministic)
 
-    def _folded(self, n_rows: int) -> bool:
-        f = self._fold_plan.get(n_rows)
-        if f is None:
-            f = self._fold_plan[n_rows] = N.step_plan(self.desc, n_rows)["folded_bn0_backward"]
-        return f
-
     def _launch(self, batch, n_rows, apply_adam: bool):
         self.ensure_batch(n_rows)
         N.set_deterministic(self.desc, self.is_deterministic())
-        defer_ok = apply_adam and not self.dp and n_rows >= 2 and self._folded(n_rows)
+        defer_ok = apply_adam and not self.dp and n_rows >= 2 and n_rows not in self._no_defer
         pending = False
         if self._late_rows:
             if defer_ok and n_rows == self._late_rows:
@@ -154,7 +148,8 @@ class FusedTrainer:
                 self.desc.flags &= ~(N.TT_FLAG_DEFER_LATE | N.TT_FLAG_LATE_PENDING)
         extra = (N.TT_FLAG_DEFER_LATE if defer else 0) | (N.TT_FLAG_LATE_PENDING if pending else 0)
         rc = call(extra)
-        if rc == N.TT_ERR_UNSUPPORTED and extra:  # geometry without the deferred form: plain step
+        if rc == N.TT_ERR_UNSUPPORTED and extra:  # geometry without the deferred form: plain steps
+            self._no_defer.add(n_rows)
             if pending:
                 self.flush()
             defer = False

@@ -943,7 +943,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   // TT_FLAG_DEFER_LATE / TT_FLAG_LATE_PENDING: single-GPU Adam steps of the
   // folded plan only (decided here, before anything is enqueued)
   const bool defer = (d->flags & TT_FLAG_DEFER_LATE) != 0, pending = (d->flags & TT_FLAG_LATE_PENDING) != 0;
-  if ((defer || pending) && (!apply_adam || x || !c.P.fold)) return TT_ERR_UNSUPPORTED;
+  if ((defer || pending) && (!apply_adam || x)) return TT_ERR_UNSUPPORTED;
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad, defer ? RED_EARLY : RED_ALL);
   r.late_mark = defer ? 1 : -1;
   if (x) {
@@ -984,7 +984,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     }
     return e;
   };
-  if (pending && !l0_late_ok(a)) return TT_ERR_UNSUPPORTED;
+  if ((defer || pending) && !l0_late_ok(a)) return TT_ERR_UNSUPPORTED;  // (nothing enqueued yet)
   LateRed late;
   if (pending) {  // the previous step's late half (same batch size: the caller flushes otherwise)
     RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
@@ -1014,7 +1014,6 @@ int32_t tt_train_flush(const tt_model_desc* d, float* params, float* buffers, in
   Ctx c;
   int rc = prepare(d, b, ws_bytes, 2, &c);
   if (rc) return rc;
-  if (!c.P.fold) return TT_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);

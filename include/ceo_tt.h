@@ -80,8 +80,8 @@ typedef struct tt_model_desc {
  *   moments or the loss are read, or a step of another batch size).  A late
  *   half runs only if the workspace records one (the step counter makes a
  *   stale LATE_PENDING a no-op on the device).  Both flags: single-GPU Adam
- *   steps (apply_adam = 1) of the folded plan (tt_step_plan info[0] = 1);
- *   otherwise TT_ERR_UNSUPPORTED, nothing enqueued.                         */
+ *   steps (apply_adam = 1) of numeric-only towers with 16-B aligned rows and
+ *   inputs up to 64 wide; otherwise TT_ERR_UNSUPPORTED, nothing enqueued.   */
 #define TT_FLAG_DEFER_LATE 2
 #define TT_FLAG_LATE_PENDING 4
 

@@ -197,3 +197,48 @@ def test_batch_size_change_and_model_reads_flush():
         ok = normwise(b[k], a[k]) < 1e-5 or np.max(np.abs(b[k] - a[k])) <= 5e-2 * 4e-4 * len(sizes)
         assert ok, (k, normwise(b[k], a[k]))
     assert N.step_plan(m.tt_desc(), 12288)["folded_bn0_backward"]
+
+
+def test_deferred_six_kernel_path_cfg2():
+    """The cfg-2 geometry (32 x 32 features, LATENT 64, B = 4096: the
+    six-kernel path, no folded BN0 backward) deferred vs plain: the same
+    training at the optimizer-scale bound, loss at 1e-5."""
+    from ceo_firm_matching import CEOFirmMatcher, Config
+    from ceo_firm_matching import _native as N
+    from ceo_firm_matching.engine import FusedTrainer
+    g = load_golden("cfg2")
+    meta = meta_of(g)
+    cfg = Config()
+    cfg.LATENT_DIM = int(g["meta/latent"])
+    cfg.DROPOUT_P = 0.1
+    cfg.DEVICE = _dev()
+    Bc, K = 4096, 5
+    rng = np.random.default_rng(12)
+    data = {
+        "firm_numeric": torch.from_numpy(rng.standard_normal((K * Bc, meta["n_firm_numeric"])).astype(np.float32)),
+        "firm_cat": torch.zeros(K * Bc, 0, dtype=torch.int64),
+        "ceo_numeric": torch.from_numpy(rng.standard_normal((K * Bc, meta["n_ceo_numeric"])).astype(np.float32)),
+        "ceo_cat": torch.zeros(K * Bc, 0, dtype=torch.int64),
+        "target": torch.from_numpy(rng.standard_normal((K * Bc, 1)).astype(np.float32)),
+        "weights": torch.from_numpy(rng.uniform(1, 10, (K * Bc, 1)).astype(np.float32)),
+    }
+    out = []
+    for defer in (False, True):
+        m = CEOFirmMatcher(meta, cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()})
+        m = m.to(_dev())
+        assert not N.step_plan(m.tt_desc(), Bc)["folded_bn0_backward"]
+        tr = FusedTrainer(m, lr=4e-4, max_batch=Bc, seed=9, deterministic=True, defer_late=defer)
+        tr.set_data({k: v.to(_dev()) for k, v in data.items()})
+        for k in range(K):
+            tr.step(None, k * Bc, Bc)
+        assert tr._late_rows == (Bc if defer else 0)
+        loss = tr.pop_loss_sum()
+        out.append(({n: q.detach().cpu().numpy().copy() for n, q in m.named_parameters()}, loss))
+    (a, la), (b, lb) = out
+    assert abs(la - lb) <= 1e-5 * abs(la)
+    for n in a:
+        if excluded_param(n):
+            continue
+        ok = normwise(b[n], a[n]) < 1e-5 or np.max(np.abs(b[n] - a[n])) <= 5e-2 * 4e-4 * K
+        assert ok, (n, normwise(b[n], a[n]))

@@ -19,5 +19,7 @@ def timeit(fn, reps=10):
 for rnd in range(2):
     for v in range(8):
         print(rnd, "variant", v, round(timeit(lambda: P.copy_probe(src.data_ptr(), dst.data_ptr(), nb, v, st)), 1))
+    for v in (8, 9):  # read-only: bytes read / time
+        print(rnd, "read variant", v, round(timeit(lambda: P.copy_probe(src.data_ptr(), dst.data_ptr(), nb, v, st)) / 2, 1))
     print(rnd, "tt_stream_copy", round(timeit(lambda: N.lib().tt_stream_copy(src.data_ptr(), dst.data_ptr(), nb, st)), 1))
     print(rnd, "torch copy_", round(timeit(lambda: dst.copy_(src)), 1))

@@ -300,11 +300,14 @@ def side_config_leg(dev, name, steps=200, warmup=20):
     with torch.cuda.graph(graph):
         for _ in range(chunk):
             tr.step_cycle(rows, B, n_batches)
+    late_after = tr.deferral_state()
     graph.replay()
+    tr.flush()  # the warm replay's last late half: outside the timed region
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps // chunk):
         graph.replay()
+    tr.after_replay(late_after)
     tr.flush()
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
@@ -598,6 +601,7 @@ def main():
             dist.barrier()
         if graph is None:
             chunk = 1
+    late_after = tr.deferral_state()  # what each captured graph's last step leaves pending
 
     tr.pop_loss_sum(read=False)
     if pg is not None:
@@ -614,6 +618,8 @@ def main():
     else:
         for _ in range(args.steps):
             step_fn()
+    if graph is not None:
+        tr.after_replay(late_after)  # the replays ran outside step(): the last one's late half is pending
     tr.flush()  # the last step's deferred late half: inside the timed region (K whole steps)
     torch.cuda.synchronize()
     if pg is not None:
@@ -734,7 +740,7 @@ def run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, 
         if pg is not None:
             tr.allreduce_and_adam()
     if defer and batch is not None:
-        tr._late_rows, tr._late_batch = B, batch
+        tr.after_replay((B, batch))
         tr.flush()
     torch.cuda.synchronize()
     plan = N.step_plan(tr.desc, B)

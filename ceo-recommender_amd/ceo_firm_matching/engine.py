@@ -177,6 +177,19 @@ class FusedTrainer:
         self._late_rows, self._late_batch = 0, None
         self.model._pending_flush = None
 
+    def deferral_state(self):
+        """The host's record of a pending late half, e.g. right after
+        capturing steps into a graph (what a replay of that graph leaves)."""
+        return (self._late_rows, self._late_batch)
+
+    def after_replay(self, state):
+        """Replaying a captured graph does not pass through step(): restore
+        the record the capture ended with, so the next flush (or step) runs the
+        last replayed step's late half.  The device guard makes a flush of
+        nothing a no-op, never a second late half."""
+        self._late_rows, self._late_batch = state
+        self.model._pending_flush = self.flush if state[0] else None
+
     def _launch_dp(self, batch, n_rows):
         """The data-parallel step: the exchange inside the step's reduction
         when the peer exchange is mapped and the reduction's blocks can all be

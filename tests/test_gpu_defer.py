@@ -242,3 +242,39 @@ def test_deferred_six_kernel_path_cfg2():
             continue
         ok = normwise(b[n], a[n]) < 1e-5 or np.max(np.abs(b[n] - a[n])) <= 5e-2 * 4e-4 * K
         assert ok, (n, normwise(b[n], a[n]))
+
+
+def test_replays_after_a_flush_keep_every_late_half():
+    """bench.py's timed region: a flush before the replays (the warm-up loss
+    read), graph replays (outside step(), so the host's pending record is
+    stale), then after_replay(the capture's final record) + flush: every
+    step's late half runs exactly once -- bitwise the same steps eager."""
+    _, _, data, make = _setup(p=0.1)
+    rows = torch.randperm(8 * B, device=_dev(), generator=torch.Generator(device=_dev()).manual_seed(4))
+    res = []
+    for use_graph in (False, True):
+        m, tr = make(True)
+        tr.step_cycle(rows, B, 8)
+        if use_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(4):
+                    tr.step_cycle(rows, B, 8)
+            st = tr.deferral_state()
+            assert st[0] == B
+            graph.replay()
+            tr.flush()  # the capture's record: runs the first replay's last late half
+            assert tr.deferral_state()[0] == 0
+            graph.replay()
+            tr.after_replay(st)
+        else:
+            for _ in range(8):
+                tr.step_cycle(rows, B, 8)
+        loss = tr.pop_loss_sum()
+        res.append((_state(m, tr), loss, tr.steps_done()))
+    (a, la, na), (b, lb, nb) = res
+    assert na == nb == 9
+    assert la == lb
+    assert np.array_equal(a, b)

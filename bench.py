@@ -282,7 +282,7 @@ def side_config_leg(dev, name, steps=200, warmup=20):
     cfg.DEVICE = dev
     torch.manual_seed(42)
     model = CEOFirmMatcher(meta, cfg).to(dev)
-    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42, defer_late=True)
+    tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42)
     tr.set_data(data)
     n_batches = n_total // B
     rows = torch.randperm(n_total, device=dev, generator=torch.Generator(device=dev).manual_seed(1000))
@@ -495,9 +495,10 @@ def main():
                     help="skip the other single-GPU config (PMC passes: counters of the headline config only)")
     ap.add_argument("--dp", action="store_true",
                     help="data-parallel step (all-reduce + Adam) even at world size 1 (tests the N>1 path)")
-    ap.add_argument("--no-defer", action="store_true",
-                    help="single GPU: keep the whole gradient reduction in each step's last kernel "
-                         "(default: its late half runs inside the next step's first kernel, TT_FLAG_DEFER_LATE)")
+    ap.add_argument("--defer", action="store_true",
+                    help="single GPU: defer the late half of each step's gradient reduction to the next step "
+                         "(TT_FLAG_DEFER_LATE; its own launch there -- DESIGN 10; default: the whole reduction "
+                         "in each step's last kernel)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -535,7 +536,7 @@ def main():
     torch.manual_seed(42)  # identical init on every rank (DDP broadcast semantics)
     model = CEOFirmMatcher(meta, cfg).to(dev)
     tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42, process_group=pg,
-                      defer_late=(pg is None and not args.no_defer))
+                      defer_late=(pg is None and args.defer))
     tr.set_data(data)
     n_batches = shard // B
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -672,7 +673,7 @@ def main():
                    "global_batch": B * world, "parallelism": f"dp{world}" if pg is not None else "single",
                    "graph": bool(graph is not None), "graph_chunk": chunk,
                    "launch": "tt_train_steps" if c_steps else ("hipgraph" if graph is not None else "eager"),
-                   "late_half": "deferred into the next step's k_l0_fwd" if tr.defer_late and not c_steps
+                   "late_half": "deferred to the next step (k_reduce_late)" if tr.defer_late and not c_steps
                                 else "in k_reduce_adam",
                    "grad_exchange": ("peer-memory one-shot inside k_reduce_adam (+ Adam)" if tr.fused_exchange
                                      else "peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
@@ -721,8 +722,8 @@ def run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, 
     torch.cuda.synchronize()
     a = tr.arena
     # the steps as the timed region ran them: with the deferred late half
-    # (TT_FLAG_DEFER_LATE) every step after the first carries the previous
-    # one's late half in its k_l0_fwd, and k_reduce_adam holds the early half
+    # (TT_FLAG_DEFER_LATE) every step after the first runs the previous one's
+    # late half ahead of its k_l0_fwd, and k_reduce_adam holds the early half
     tr.flush()
     defer = tr.defer_late and pg is None
     batch = None

@@ -186,11 +186,10 @@ static std::once_flag g_attr_once;
 static void set_lds_attrs() {
   std::call_once(g_attr_once, [] {
     const int mx = (int)LDS_MAX;
-    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true, false>, (const void*)k_l0_fwd<ROWS, 1, false, false>,
-                        (const void*)k_l0_fwd<ROWS, 2, true, false>, (const void*)k_l0_fwd<ROWS, 2, false, false>,
-                        (const void*)k_l0_fwd<ROWS, 4, true, false>, (const void*)k_l0_fwd<ROWS, 4, false, false>,
-                        (const void*)k_l0_fwd<ROWS, 8, true, false>, (const void*)k_l0_fwd<ROWS, 8, false, false>,
-                        (const void*)k_l0_fwd<ROWS, 1, true, true>, (const void*)k_l0_fwd<ROWS, 2, true, true>,
+    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true>, (const void*)k_l0_fwd<ROWS, 1, false>,
+                        (const void*)k_l0_fwd<ROWS, 2, true>, (const void*)k_l0_fwd<ROWS, 2, false>,
+                        (const void*)k_l0_fwd<ROWS, 4, true>, (const void*)k_l0_fwd<ROWS, 4, false>,
+                        (const void*)k_l0_fwd<ROWS, 8, true>, (const void*)k_l0_fwd<ROWS, 8, false>,
                         (const void*)k_l4_fwd<ROWS>,
                         (const void*)k_top<4, 64, false>, (const void*)k_top<8, 64, false>,
                         (const void*)k_top<4, 128, false>, (const void*)k_top<8, 128, false>,
@@ -382,7 +381,6 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.tgw = ws + W.tgw;
   a.det = (d->flags & TT_FLAG_DETERMINISTIC) ? 1 : 0;
   a.xcd_pair = fold ? 1 : 0;  // 64-row tiles on the XCD of the fold kernel's 128-row tile (tile64)
-  a.l0_gx = (int)(padded_rows(b->n_rows) / ROWS);  // k_l0_fwd's row-tile blocks (Plan::n_tiles)
   a.dslot_lsr = ws + W.det_lsr;
 }
 
@@ -528,10 +526,6 @@ static LateRed to_late(const RedArgs& r) {
   }
   return q;
 }
-// k_l0_fwd blocks per tower row (y) that carry a late half: half of its
-// element blocks each, rounded to 8 so the row tiles keep their XCDs
-static int late_gx(const LateRed& q) { return (int)round_up((q.vn / RED_E + 1) / 2, 8); }
-
 static int launch_check() {
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? TT_OK : (int)e;
@@ -571,35 +565,19 @@ static void launch(K kern, dim3 g, dim3 b, size_t lds, hipStream_t s, Evs ev, A.
     hipLaunchKernelGGL(kern, g, b, lds, s, args...);
 }
 
-// k_l0_fwd's instance for this step, or -1 when a deferred late half rides
-// along (late != NULL) and no LATE instance covers the geometry
-static int l0_late_ok(const StepArgs& a) {
-  return a.tw[0].num_vec && a.tw[1].num_vec && l0_ks(std::max(a.tw[0].kp, a.tw[1].kp)) <= 2;
-}
-static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}, const LateRed* late = nullptr) {
+static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
   // instance by the widest tower input (32-wide K steps held in registers)
   // and whether both towers take the aligned numeric-only gather
   const int ks = l0_ks(std::max(a.tw[0].kp, a.tw[1].kp));
   const bool vec = a.tw[0].num_vec && a.tw[1].num_vec;
-  const dim3 blk(4 * ROWS);
-  LateRed none;
-  std::memset(&none, 0, sizeof(none));
-  if (late) {  // the caller checked l0_late_ok
-    const dim3 grid(P.n_tiles + late_gx(*late), 2);
-    if (ks == 1)
-      launch(k_l0_fwd<ROWS, 1, true, true>, grid, blk, P.lds_l0, s, ev, a, *late);
-    else
-      launch(k_l0_fwd<ROWS, 2, true, true>, grid, blk, P.lds_l0, s, ev, a, *late);
-    return;
-  }
-  const dim3 grid(P.n_tiles, 2);
-#define TT_L0(KS)                                                                   \
-  if (ks == KS) {                                                                   \
-    if (vec)                                                                        \
-      launch(k_l0_fwd<ROWS, KS, true, false>, grid, blk, P.lds_l0, s, ev, a, none); \
-    else                                                                            \
-      launch(k_l0_fwd<ROWS, KS, false, false>, grid, blk, P.lds_l0, s, ev, a, none);\
-    return;                                                                         \
+  const dim3 blk(4 * ROWS), grid(P.n_tiles, 2);
+#define TT_L0(KS)                                                             \
+  if (ks == KS) {                                                             \
+    if (vec)                                                                  \
+      launch(k_l0_fwd<ROWS, KS, true>, grid, blk, P.lds_l0, s, ev, a);        \
+    else                                                                      \
+      launch(k_l0_fwd<ROWS, KS, false>, grid, blk, P.lds_l0, s, ev, a);       \
+    return;                                                                   \
   }
   TT_L0(1)
   TT_L0(2)
@@ -984,14 +962,18 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     }
     return e;
   };
-  if ((defer || pending) && !l0_late_ok(a)) return TT_ERR_UNSUPPORTED;  // (nothing enqueued yet)
-  LateRed late;
-  if (pending) {  // the previous step's late half (same batch size: the caller flushes otherwise)
+  if (pending) {
+    // the previous step's late half (same batch size: the caller flushes
+    // otherwise), as its own launch ahead of this step's first kernel.  (It
+    // was built as extra workgroups of k_l0_fwd; that instance faulted on the
+    // GPU even with its row tiles and late blocks compiled out -- DESIGN 10 --
+    // and was removed.)
     RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
     red_step_fields(lr, RED_LATE, c.W, w, b->n_rows, state, 1, params, exp_avg, exp_avg_sq, hp, a.adam_slots);
-    late = to_late(lr);
+    const LateRed late = to_late(lr);
+    hipLaunchKernelGGL(k_reduce_late, dim3((unsigned)(late.vn / RED_E)), dim3(RED_E * LATE_G), 0, s, late);
   }
-  launch_l0(a, c.P, s, ev(0), pending ? &late : nullptr);
+  launch_l0(a, c.P, s, ev(0));
   det_fold(a, c.P, DET_L0, s);
   launch_l4(a, c.P, s, ev(1));
   det_fold(a, c.P, DET_L4, s);

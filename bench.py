@@ -496,9 +496,9 @@ def main():
     ap.add_argument("--dp", action="store_true",
                     help="data-parallel step (all-reduce + Adam) even at world size 1 (tests the N>1 path)")
     ap.add_argument("--defer", action="store_true",
-                    help="single GPU: defer the late half of each step's gradient reduction to the next step "
-                         "(TT_FLAG_DEFER_LATE; its own launch there -- DESIGN 10; default: the whole reduction "
-                         "in each step's last kernel)")
+                    help="single GPU: the late half of each step's gradient reduction runs inside the next "
+                         "step's first kernel (TT_FLAG_DEFER_LATE; default: the whole reduction in each step's "
+                         "last kernel)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -673,7 +673,7 @@ def main():
                    "global_batch": B * world, "parallelism": f"dp{world}" if pg is not None else "single",
                    "graph": bool(graph is not None), "graph_chunk": chunk,
                    "launch": "tt_train_steps" if c_steps else ("hipgraph" if graph is not None else "eager"),
-                   "late_half": "deferred to the next step (k_reduce_late)" if tr.defer_late and not c_steps
+                   "late_half": "deferred into the next step's k_l0_fwd" if tr.defer_late and not c_steps
                                 else "in k_reduce_adam",
                    "grad_exchange": ("peer-memory one-shot inside k_reduce_adam (+ Adam)" if tr.fused_exchange
                                      else "peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
@@ -722,8 +722,8 @@ def run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, 
     torch.cuda.synchronize()
     a = tr.arena
     # the steps as the timed region ran them: with the deferred late half
-    # (TT_FLAG_DEFER_LATE) every step after the first runs the previous one's
-    # late half ahead of its k_l0_fwd, and k_reduce_adam holds the early half
+    # (TT_FLAG_DEFER_LATE) every step after the first carries the previous
+    # one's late half in its k_l0_fwd, and k_reduce_adam holds the early half
     tr.flush()
     defer = tr.defer_late and pg is None
     batch = None

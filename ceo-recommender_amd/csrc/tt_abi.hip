@@ -186,10 +186,11 @@ static std::once_flag g_attr_once;
 static void set_lds_attrs() {
   std::call_once(g_attr_once, [] {
     const int mx = (int)LDS_MAX;
-    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true>, (const void*)k_l0_fwd<ROWS, 1, false>,
-                        (const void*)k_l0_fwd<ROWS, 2, true>, (const void*)k_l0_fwd<ROWS, 2, false>,
-                        (const void*)k_l0_fwd<ROWS, 4, true>, (const void*)k_l0_fwd<ROWS, 4, false>,
-                        (const void*)k_l0_fwd<ROWS, 8, true>, (const void*)k_l0_fwd<ROWS, 8, false>,
+    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true, false>, (const void*)k_l0_fwd<ROWS, 1, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 2, true, false>, (const void*)k_l0_fwd<ROWS, 2, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 4, true, false>, (const void*)k_l0_fwd<ROWS, 4, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 8, true, false>, (const void*)k_l0_fwd<ROWS, 8, false, false>,
+                        (const void*)k_l0_fwd<ROWS, 1, true, true>, (const void*)k_l0_fwd<ROWS, 2, true, true>,
                         (const void*)k_l4_fwd<ROWS>,
                         (const void*)k_top<4, 64, false>, (const void*)k_top<8, 64, false>,
                         (const void*)k_top<4, 128, false>, (const void*)k_top<8, 128, false>,
@@ -381,6 +382,7 @@ static void fill_args(StepArgs& a, const tt_model_desc* d, const Layout& L, cons
   a.tgw = ws + W.tgw;
   a.det = (d->flags & TT_FLAG_DETERMINISTIC) ? 1 : 0;
   a.xcd_pair = fold ? 1 : 0;  // 64-row tiles on the XCD of the fold kernel's 128-row tile (tile64)
+  a.l0_gx = (int)(padded_rows(b->n_rows) / ROWS);  // k_l0_fwd's row-tile blocks (Plan::n_tiles)
   a.dslot_lsr = ws + W.det_lsr;
 }
 
@@ -400,10 +402,11 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   int k = 0;
   bool late_range = false;  // set around the late ranges below
   const int G = part == RED_LATE ? LATE_G : RED_G;
+  // returns whether the range went into this part's segment list
   auto add = [&](int64_t off, int64_t len, int kind, int tower, int64_t so, int n_slabs, float* rep = nullptr,
-                 int64_t rep_stride = 0) {
-    if (len <= 0) return;
-    if ((part == RED_EARLY && late_range) || (part == RED_LATE && !late_range)) return;
+                 int64_t rep_stride = 0) -> bool {
+    if (len <= 0) return false;
+    if ((part == RED_EARLY && late_range) || (part == RED_LATE && !late_range)) return false;
     r.seg[k].off = off;
     r.seg[k].len = len;
     r.seg[k].kind = kind;
@@ -413,6 +416,7 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     r.seg[k].rep = rep;
     r.seg[k].rep_stride = rep_stride;
     ++k;
+    return true;
   };
   int64_t emb_total = L.slot[0][TT_SLOT_W0];
   add(0, emb_total, 1, 0, 0, 0);
@@ -423,16 +427,21 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
     if (P.fold) {
       float* fr = ws + W.fr + (int64_t)t * NREP * FRW;
       for (int kind = 3; kind <= 4; ++kind) {
-        add(s[kind == 3 ? TT_SLOT_W0 : TT_SLOT_B0], kind == 3 ? (int64_t)H0 * L.in_dim[t] : H0, kind, t,
-            L.so[t][0], P.n_tiles_mid, fr, FRW);
+        // only when added: in a late-half list nothing is, and seg[k - 1] is
+        // then another range -- or, at k = 0, the caller's stack before the
+        // struct (that write corrupted the pending step's kernel arguments:
+        // GPU faults at the first deferred step; tests/native/abi_host_check)
+        if (!add(s[kind == 3 ? TT_SLOT_W0 : TT_SLOT_B0], kind == 3 ? (int64_t)H0 * L.in_dim[t] : H0, kind, t,
+                 L.so[t][0], P.n_tiles_mid, fr, FRW))
+          continue;
         Seg& g = r.seg[k - 1];
         g.in = L.in_dim[t];
         g.kp = L.kp[t];
         g.k0 = ws + W.k0s[t];
         g.xsh = ws + W.xsh[t];
       }
-      add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, fr, FRW);
-      r.seg[k - 1].keep = 1;  // zeroed by the next step's k_l0_fwd
+      if (add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, fr, FRW))
+        r.seg[k - 1].keep = 1;  // zeroed by the next step's k_l0_fwd
     } else {
       // W0 and b0 apart: the slab's W0 range may be sized for the folded P | Q
       add(s[TT_SLOT_W0], (int64_t)H0 * L.in_dim[t], 0, t, L.so[t][0], P.n_tiles);
@@ -526,6 +535,10 @@ static LateRed to_late(const RedArgs& r) {
   }
   return q;
 }
+// k_l0_fwd blocks per tower row (y) that carry a late half: half of its
+// element blocks each, rounded to 8 so the row tiles keep their XCDs
+static int late_gx(const LateRed& q) { return (int)round_up((q.vn / RED_E + 1) / 2, 8); }
+
 static int launch_check() {
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? TT_OK : (int)e;
@@ -565,19 +578,35 @@ static void launch(K kern, dim3 g, dim3 b, size_t lds, hipStream_t s, Evs ev, A.
     hipLaunchKernelGGL(kern, g, b, lds, s, args...);
 }
 
-static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
+// k_l0_fwd's instance for this step, or -1 when a deferred late half rides
+// along (late != NULL) and no LATE instance covers the geometry
+static int l0_late_ok(const StepArgs& a) {
+  return a.tw[0].num_vec && a.tw[1].num_vec && l0_ks(std::max(a.tw[0].kp, a.tw[1].kp)) <= 2;
+}
+static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}, const LateRed* late = nullptr) {
   // instance by the widest tower input (32-wide K steps held in registers)
   // and whether both towers take the aligned numeric-only gather
   const int ks = l0_ks(std::max(a.tw[0].kp, a.tw[1].kp));
   const bool vec = a.tw[0].num_vec && a.tw[1].num_vec;
-  const dim3 blk(4 * ROWS), grid(P.n_tiles, 2);
-#define TT_L0(KS)                                                             \
-  if (ks == KS) {                                                             \
-    if (vec)                                                                  \
-      launch(k_l0_fwd<ROWS, KS, true>, grid, blk, P.lds_l0, s, ev, a);        \
-    else                                                                      \
-      launch(k_l0_fwd<ROWS, KS, false>, grid, blk, P.lds_l0, s, ev, a);       \
-    return;                                                                   \
+  const dim3 blk(4 * ROWS);
+  LateRed none;
+  std::memset(&none, 0, sizeof(none));
+  if (late) {  // the caller checked l0_late_ok
+    const dim3 grid(P.n_tiles + late_gx(*late), 2);
+    if (ks == 1)
+      launch(k_l0_fwd<ROWS, 1, true, true>, grid, blk, P.lds_l0, s, ev, a, *late);
+    else
+      launch(k_l0_fwd<ROWS, 2, true, true>, grid, blk, P.lds_l0, s, ev, a, *late);
+    return;
+  }
+  const dim3 grid(P.n_tiles, 2);
+#define TT_L0(KS)                                                                   \
+  if (ks == KS) {                                                                   \
+    if (vec)                                                                        \
+      launch(k_l0_fwd<ROWS, KS, true, false>, grid, blk, P.lds_l0, s, ev, a, none); \
+    else                                                                            \
+      launch(k_l0_fwd<ROWS, KS, false, false>, grid, blk, P.lds_l0, s, ev, a, none);\
+    return;                                                                         \
   }
   TT_L0(1)
   TT_L0(2)
@@ -962,18 +991,14 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     }
     return e;
   };
-  if (pending) {
-    // the previous step's late half (same batch size: the caller flushes
-    // otherwise), as its own launch ahead of this step's first kernel.  (It
-    // was built as extra workgroups of k_l0_fwd; that instance faulted on the
-    // GPU even with its row tiles and late blocks compiled out -- DESIGN 10 --
-    // and was removed.)
+  if ((defer || pending) && !l0_late_ok(a)) return TT_ERR_UNSUPPORTED;  // (nothing enqueued yet)
+  LateRed late;
+  if (pending) {  // the previous step's late half (same batch size: the caller flushes otherwise)
     RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
     red_step_fields(lr, RED_LATE, c.W, w, b->n_rows, state, 1, params, exp_avg, exp_avg_sq, hp, a.adam_slots);
-    const LateRed late = to_late(lr);
-    hipLaunchKernelGGL(k_reduce_late, dim3((unsigned)(late.vn / RED_E)), dim3(RED_E * LATE_G), 0, s, late);
+    late = to_late(lr);
   }
-  launch_l0(a, c.P, s, ev(0));
+  launch_l0(a, c.P, s, ev(0), pending ? &late : nullptr);
   det_fold(a, c.P, DET_L0, s);
   launch_l4(a, c.P, s, ev(1));
   det_fold(a, c.P, DET_L4, s);

@@ -453,6 +453,7 @@ struct StepArgs {
   int det;               // deterministic reductions (TT_FLAG_DETERMINISTIC): slots + k_det_fold
   float* dslot_lsr;      // det: per-block (dls, loss) partials [blocks][2]
   int xcd_pair;          // folded step: 64-row kernels take XCD-paired tiles (tile64)
+  int l0_gx;             // k_l0_fwd's row-tile blocks along x (more blocks: a deferred late half)
 };
 
 // Row tile of a 64-row kernel's block (k_l0_fwd, k_l4_fwd, k_top_pair).
@@ -759,7 +760,7 @@ struct RedExchange {
 };
 
 // NS: segment capacity (the whole arena: MAX_SEG; a deferred late half,
-// LateRed below: MAX_LATE_SEG)
+// LateRed below: MAX_LATE_SEG -- it rides in k_l0_fwd's kernel arguments)
 template <int NS>
 struct RedArgsN {
   Seg seg[NS];
@@ -795,6 +796,6 @@ struct RedArgsN {
 using RedArgs = RedArgsN<MAX_SEG>;
 constexpr int MAX_LATE_SEG = 8;
 using LateRed = RedArgsN<MAX_LATE_SEG>;
-constexpr int LATE_G = 4;  // slab groups of a late-half block (k_reduce_late: 64 elements x 4)
+constexpr int LATE_G = 4;  // slab groups of a late-half block: 64 elements x 4 = k_l0_fwd's 256 threads
 
 }  // namespace tt

@@ -36,9 +36,9 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   reduce_body<RedArgs, RED_G, PRE, EX, false>(a, (int)blockIdx.x, part, xpart, &xok_s);
 }
 
-// A deferred late half (TT_FLAG_DEFER_LATE): run by the next step ahead of
-// its first kernel (TT_FLAG_LATE_PENDING) or by tt_train_flush -- one body
-// and summation order, so both give the same bits.
+// A deferred late half on its own (tt_train_flush): the same LATE_G body and
+// summation order as inside k_l0_fwd, so flushed and in-step late halves
+// give the same bits.
 __global__ __launch_bounds__(RED_E* LATE_G) void k_reduce_late(LateRed a) {
   __shared__ float part[LATE_G * RED_E];
   __shared__ float xpart[4 * LATE_G * RED_E];

@@ -1,5 +1,5 @@
-// Gradient reduction body shared by k_reduce_adam and the deferred late half
-// (k_reduce_late), tt_optim.hip.
+// Gradient reduction body shared by k_reduce_adam (tt_optim.hip) and the
+// deferred late half inside k_l0_fwd (tt_tower.hip).  See tt_optim.hip.
 #pragma once
 #include "tt_common.h"
 
@@ -58,7 +58,7 @@ __device__ __forceinline__ bool reduce_exchange(const RedExchange& X, int64_t t,
 // The reduction body for one element block `bid` (RED_E elements x G slab
 // groups = the block's threads).  k_reduce_adam runs it at G = G; a
 // deferred late half (LATE, tt_train_step with TT_FLAG_DEFER_LATE) runs it at
-// G = LATE_G (k_reduce_late: the next step or tt_train_flush).  LDS:
+// G = LATE_G inside the next step's k_l0_fwd or in tt_train_flush.  LDS:
 // part [G][RED_E], xpart [4][G][RED_E] floats, *xok_s.
 template <class A, int G, bool PRE, bool EX, bool LATE>
 __device__ __forceinline__ void reduce_body(const A& a, int bid, float* part, float* xpart, int* xok_ptr) {
@@ -71,8 +71,8 @@ __device__ __forceinline__ void reduce_body(const A& a, int bid, float* part, fl
   // the step first: a later load would make its wait (in-order vmcnt) wait for the slabs
   // (a select of the two addresses: one FLAT load, issued first -- measured
   // 0.2 us faster here than the global load the tower kernels use).  A late
-  // half takes step_done (its early half's step; step_cur may already be the
-  // next step's)
+  // half takes step_done (its early half's step): the next step's k_l0_fwd
+  // rewrites step_cur meanwhile
   int64_t t;
   if constexpr (LATE) {
     t = a.state->step_done;

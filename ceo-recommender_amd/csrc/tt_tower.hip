@@ -32,6 +32,7 @@
 //    for loads, the workspace is padded to whole tiles so per-row stores need
 //    no guard, and rows beyond B are masked out of statistics with selects.
 #include "tt_common.h"
+#include "tt_reduce.h"
 
 namespace tt {
 
@@ -372,13 +373,26 @@ __device__ __forceinline__ void zero_x8(const TowerDev& T, int c0, float (&x)[8]
   }
 }
 
-template <int R, int KS, bool VEC>
-__global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) {
+// LATE: blocks x >= a.l0_gx run the previous step's deferred late half of
+// the gradient reduction (TT_FLAG_DEFER_LATE: W4, BN1 affine, W8, b8,
+// logit_scale and the loss fold) beside the row tiles -- none of which reads
+// or writes what this kernel does.
+template <int R, int KS, bool VEC, bool LATE>
+__global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, LateRed late) {
   constexpr int NTH = R * 4;
   constexpr int KC = 32 * KS, LDK = L0Lds<R>::ldk(KS), PL = H0 * LDK;
   constexpr int C4N = KC / 4, N4 = H0 * C4N, WPT = N4 / NTH;  // W0 float4 per thread
   static_assert(R == 64 && N4 % NTH == 0, "4 waves x 16 rows");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if constexpr (LATE) {
+    static_assert(LATE_G * RED_E == NTH, "a late-half block is one k_l0_fwd block");
+    if ((int)blockIdx.x >= a.l0_gx) {
+      const int bid = ((int)blockIdx.x - a.l0_gx) * 2 + (int)blockIdx.y;
+      reduce_body<LateRed, LATE_G, true, false, true>(late, bid, smem, smem + LATE_G * RED_E,
+                                                      reinterpret_cast<int*>(smem + 5 * LATE_G * RED_E));
+      return;
+    }
+  }
   const int t = blockIdx.y;
   const TowerDev& T = a.tw[t];
   const int64_t step = step_for_first_kernel(a);
@@ -522,9 +536,9 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a) 
   }
   // the folded BN0 backward's replicas start every step at zero (k_bwd_mid
   // accumulates them, k_reduce_adam only reads them)
-  if (a.fr_zero) {
-    const int nthr = (int)(gridDim.x * gridDim.y) * NTH;
-    for (int i = (int)((blockIdx.y * gridDim.x + blockIdx.x) * NTH + threadIdx.x); i < a.fr_zero_len; i += nthr)
+  if (a.fr_zero) {  // (the row-tile blocks only: l0_gx, not gridDim.x)
+    const int nthr = a.l0_gx * (int)gridDim.y * NTH;
+    for (int i = (int)((blockIdx.y * a.l0_gx + blockIdx.x) * NTH + threadIdx.x); i < a.fr_zero_len; i += nthr)
       a.fr_zero[i] = 0.f;
   }
   TT_STAMP(0, 3);
@@ -2350,13 +2364,15 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   TT_STAMP(4, 3);
 }
 
-#define TT_L0(KS) template __global__ void k_l0_fwd<64, KS, true>(StepArgs); \
-  template __global__ void k_l0_fwd<64, KS, false>(StepArgs);
+#define TT_L0(KS) template __global__ void k_l0_fwd<64, KS, true, false>(StepArgs, LateRed); \
+  template __global__ void k_l0_fwd<64, KS, false, false>(StepArgs, LateRed);
 TT_L0(1)
 TT_L0(2)
 TT_L0(4)
 TT_L0(8)
 #undef TT_L0
+template __global__ void k_l0_fwd<64, 1, true, true>(StepArgs, LateRed);
+template __global__ void k_l0_fwd<64, 2, true, true>(StepArgs, LateRed);
 template __global__ void k_l4_fwd<64>(StepArgs);
 template __global__ void k_top_pair<4>(StepArgs);
 template __global__ void k_top_pair<8>(StepArgs);

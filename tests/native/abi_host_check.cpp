@@ -93,6 +93,26 @@ int main() {
     nob.num[0] = nullptr;
     if (d.n_num[0] > 0) CHECK(tt_forward(&d, p, p, nbt, &nob, 0, 0, 1, p, 1 << 30, p, nullptr) == TT_ERR_ARG);
   }
+  // the deferred late half's host planning (make_red for the late part of the
+  // reduction, tt_train_flush / TT_FLAG_LATE_PENDING) on the cfg-3 geometry:
+  // everything up to the launch is host code (without a GPU the launches
+  // themselves fail, which is all right here); ASan checks the segment lists
+  {
+    tt_model_desc d = desc(64, 64, {}, {}, 128);
+    std::vector<float> big(64 * 16384);
+    float* p = big.data();
+    tt_batch bt;
+    std::memset(&bt, 0, sizeof(bt));
+    bt.n_rows = 16384;
+    bt.num[0] = bt.num[1] = p;
+    bt.num_ld[0] = bt.num_ld[1] = 64;
+    int64_t nbt[4] = {0, 0, 0, 0};
+    tt_adam_hp hp = {4e-4f, 0.9f, 0.999f, 1e-8f};
+    const int64_t ws = tt_workspace_bytes(&d, 16384);
+    (void)tt_train_flush(&d, p, p, nbt, &bt, &hp, reinterpret_cast<tt_state*>(p), p, ws, p, p, p, nullptr);
+    d.flags |= TT_FLAG_DEFER_LATE | TT_FLAG_LATE_PENDING;
+    (void)tt_train_step(&d, p, p, nbt, &bt, &hp, 0, reinterpret_cast<tt_state*>(p), p, ws, p, p, p, 1, nullptr);
+  }
   // unsupported shapes
   tt_model_desc big = desc(64, 64, {}, {}, 1024);
   int32_t info[6];

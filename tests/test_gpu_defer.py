@@ -1,7 +1,7 @@
 """Deferred late half of the gradient reduction (TT_FLAG_DEFER_LATE,
 DESIGN 10): a step's W4 / BN1-affine / W8 / logit_scale reduction + Adam and
-its loss fold run at the start of the NEXT step (k_reduce_late ahead of its
-first kernel) or in tt_train_flush.
+its loss fold run inside the NEXT step's first kernel (or in tt_train_flush),
+so the step keeps five launches and that work leaves the critical path.
 
 * K deferred steps back to back, then the flush: the same training as K
   plain steps (training.py:44-57) -- parameters, Adam moments, BN buffers

@@ -163,9 +163,12 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
     W.dY1[t] = take(rows * H1);
   }
   W.tgw = take(rows * 2);
-  for (int t = 0; t < 2; ++t) W.slab[t] = take((int64_t)W.n_tiles * L.slab_ld);
-  for (int t = 0; t < 2; ++t) W.det[t] = take((int64_t)W.n_tiles * DET_W);
-  W.det_lsr = take((int64_t)W.n_tiles * 2);
+  // slab / deterministic-slot rows: one per 64-row tile, or per 32-row
+  // k_top_pair tile of a batch below TT_PAIR32_MAX_B (twice as many)
+  const int64_t srows = std::max<int64_t>(W.n_tiles, std::min<int64_t>(2 * W.n_tiles, 2 * (TT_PAIR32_MAX_B / ROWS) + 2));
+  for (int t = 0; t < 2; ++t) W.slab[t] = take(srows * L.slab_ld);
+  for (int t = 0; t < 2; ++t) W.det[t] = take(srows * DET_W);
+  W.det_lsr = take(srows * 2);
   for (int t = 0; t < 2; ++t) {
     const int ew = L.in_dim[t] - L.n_num[t];
     W.demb[t] = ew > 0 ? take(rows * ew) : -1;
@@ -196,7 +199,8 @@ static void set_lds_attrs() {
                         (const void*)k_top<4, 128, false>, (const void*)k_top<8, 128, false>,
                         (const void*)k_top<4, 64, true>,  (const void*)k_top<8, 64, true>,
                         (const void*)k_top<4, 128, true>, (const void*)k_top<8, 128, true>,
-                        (const void*)k_top_pair<4>, (const void*)k_top_pair<8>,
+                        (const void*)k_top_pair<4, 64>, (const void*)k_top_pair<8, 64>,
+                        (const void*)k_top_pair<4, 32>, (const void*)k_top_pair<8, 32>,
                         (const void*)k_bwd_mid<ROWS>, (const void*)k_bwd_mid_fold<FOLD_ROWS, true>,
                         (const void*)k_bwd_mid_fold<FOLD_ROWS, false>, (const void*)k_bwd_first<ROWS>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
@@ -207,7 +211,9 @@ static void set_lds_attrs() {
 
 struct Plan {
   size_t lds_l0, lds_l4, lds_top, lds_mid, lds_first, lds_pair;
-  bool top_pair;    // training steps run k_top_pair (both towers per 64-row block)
+  bool top_pair;    // training steps run k_top_pair (both towers per block)
+  int pair_rows;    // its rows per block: 64, or 32 below the folded path (twice the blocks)
+  int n_tiles_pair; // its tiles (a training step's k_top slab count)
   int ndt;
   int top_rows;     // row tile of k_top (64, or 128 for large batches)
   int n_tiles;      // 64-row tiles
@@ -251,7 +257,12 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   const int tl = P->ndt == 4 ? (P->top_rows == 64 ? TopLds<4, 64>::total : TopLds<4, 128>::total)
                              : (P->top_rows == 64 ? TopLds<8, 64>::total : TopLds<8, 128>::total);
   P->lds_top = sizeof(float) * (size_t)tl;
-  P->lds_pair = sizeof(float) * (size_t)(P->ndt == 4 ? PairLds<4>::total : PairLds<8>::total);
+  // below the folded path the 64-row k_top_pair leaves CUs idle (cfg 2: 64
+  // blocks on 256 CUs): 32-row blocks there (TT_PAIR32_MAX_B = 0: never)
+  P->pair_rows = P->top_pair && !P->fold && B < TT_PAIR32_MAX_B ? 32 : 64;
+  P->n_tiles_pair = (int)((P->n_tiles * ROWS) / P->pair_rows);
+  P->lds_pair = sizeof(float) * (size_t)(P->pair_rows == 32 ? (P->ndt == 4 ? PairLds<4, 32>::total : PairLds<8, 32>::total)
+                                                            : (P->ndt == 4 ? PairLds<4>::total : PairLds<8>::total));
   P->lds_mid = P->fold ? FoldLds<FOLD_ROWS>::bytes : MidLds<ROWS>::bytes;
   P->lds_first = FirstLds<ROWS>::bytes(kpm);
   P->lds_gen_fwd = gen_fwd_lds(d->latent);
@@ -544,6 +555,12 @@ static int launch_check() {
   return e == hipSuccess ? TT_OK : (int)e;
 }
 
+// A training step's k_top is k_top_pair (from B = 4096): its tiles are the
+// W8 / b8 slab count of the step's reduction and deterministic fold
+static void pair_plan(Plan* P) {
+  if (P->top_pair) P->n_tiles_top = P->n_tiles_pair;
+}
+
 struct Ctx {
   Layout L;
   WsLayout W;
@@ -726,11 +743,19 @@ static void launch_top(const StepArgs& a, const Plan& P, int grid_y, hipStream_t
     (void)ev;
     return;
   }
-  if (a.mode == TOP_TRAIN && P.top_pair) {
-    if (P.ndt == 4)
-      launch(k_top_pair<4>, dim3(P.n_tiles_top), dim3(512), P.lds_pair, s, ev, a);
-    else
-      launch(k_top_pair<8>, dim3(P.n_tiles_top), dim3(512), P.lds_pair, s, ev, a);
+  if (a.mode == TOP_TRAIN && P.top_pair) {  // (training steps set n_tiles_top = n_tiles_pair: pair_plan)
+    const dim3 g(P.n_tiles_pair), b(8 * P.pair_rows);
+    if (P.pair_rows == 32) {
+      if (P.ndt == 4)
+        launch(k_top_pair<4, 32>, g, b, P.lds_pair, s, ev, a);
+      else
+        launch(k_top_pair<8, 32>, g, b, P.lds_pair, s, ev, a);
+    } else {
+      if (P.ndt == 4)
+        launch(k_top_pair<4, 64>, g, b, P.lds_pair, s, ev, a);
+      else
+        launch(k_top_pair<8, 64>, g, b, P.lds_pair, s, ev, a);
+    }
     return;
   }
   if (a.mode == TOP_EMB_FWD || a.mode == TOP_EMB_BWD)
@@ -945,6 +970,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   Ctx c;
   int rc = prepare(d, b, ws_bytes, 2, &c);
   if (rc) return rc;
+  pair_plan(&c.P);
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   // TT_FLAG_DEFER_LATE / TT_FLAG_LATE_PENDING: single-GPU Adam steps of the
@@ -1021,6 +1047,7 @@ int32_t tt_train_flush(const tt_model_desc* d, float* params, float* buffers, in
   Ctx c;
   int rc = prepare(d, b, ws_bytes, 2, &c);
   if (rc) return rc;
+  pair_plan(&c.P);
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
@@ -1103,7 +1130,13 @@ static int cosine_launch(const float* u, const float* v, const float* tg, const 
   if (B == 0) return TT_OK;
   const bool vec0 = (D % 4 == 0);
   const int64_t rows_per_block = vec0 ? COS_ROWS_PER_BLOCK : COS_ROWS_PER_BLOCK_ITER;
-  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((B + rows_per_block - 1) / rows_per_block, 4096));
+  // at most 16,384 blocks: at B = 4M, D = 128 each loops 8 times over its
+  // rows (the next rows prefetched) and ends with the two loss / dls
+  // atomics.  Probed with the two sums in one line, as bench.py and the
+  // tests pass them (tools/cosprobe): 1,024-4,096 blocks 5.07-5.26 TB/s
+  // (4,096: a partial last wave of blocks), 16,384 5.41, 65,536 4.53 (the
+  // atomics on one line serialise)
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((B + rows_per_block - 1) / rows_per_block, 16384));
   const dim3 g(nb), t(256);
   const bool vec = (D % 4 == 0) && ((uintptr_t)u % 16 == 0) && ((uintptr_t)v % 16 == 0) &&
                    (!bwd || ((uintptr_t)du % 16 == 0 && (uintptr_t)dv % 16 == 0));
@@ -1152,11 +1185,14 @@ int32_t tt_stream_copy(const void* src, void* dst, int64_t bytes, tt_stream_t st
   if (!src || !dst || bytes < 0 || bytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16) return TT_ERR_ARG;
   const int64_t n4 = bytes / 16;
   if (n4 == 0) return TT_OK;
-  // 8 blocks per CU of 256 threads: enough loads in flight to saturate HBM
-  const int64_t want = (n4 + COPY_THREADS * COPY_UNROLL - 1) / (COPY_THREADS * COPY_UNROLL);
-  const int grid = (int)std::min<int64_t>(want, 256 * 8);
-  hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(COPY_THREADS), 0, (hipStream_t)stream,
-                     (const float4*)src, (float4*)dst, n4);
+  // one float4 per thread, contiguous blocks (k_stream_copy); launched in
+  // pieces of at most 2^31 - 1 blocks
+  const int64_t per = (int64_t)0x7FFFFFFF * COPY_THREADS;
+  for (int64_t o = 0; o < n4; o += per) {
+    const int64_t m = std::min(per, n4 - o);
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((m + COPY_THREADS - 1) / COPY_THREADS)), dim3(COPY_THREADS), 0,
+                       (hipStream_t)stream, (const float4*)src + o, (float4*)dst + o, m);
+  }
   return (int32_t)hipGetLastError();
 }
 

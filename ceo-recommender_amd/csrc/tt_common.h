@@ -30,6 +30,9 @@ constexpr int BNG = 2 * H0 + 2 * H1;  // one replica of a tower's BN-affine grad
 constexpr int FRW = 3 * H0 + 64;
 constexpr int FOLD_MAX_KP = 64;
 constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
+#ifndef TT_PAIR32_MAX_B
+#define TT_PAIR32_MAX_B 8192  // training batches below it (and unfolded) run k_top_pair on 32-row blocks
+#endif
 #ifndef TT_FOLD_MIN_B
 #define TT_FOLD_MIN_B 8192  // smallest batch that runs the folded BN0 backward
 #endif

@@ -188,25 +188,22 @@ __global__ __launch_bounds__(COS_THREADS) void k_cosine_scalar(const float* __re
 
 
 
-// HBM stream probe (tt_stream_copy): 16-B loads and stores, each thread
-// issues its UNROLL loads before any store, grid-stride over the buffer --
-// the same access shape as k_cosine's row streams, so its rate is the
-// ceiling that kernel is quoted against (bench.py cosine_roofline).
+// HBM stream ceiling (tt_stream_copy): one 16-B nontemporal load and store
+// per thread, each block a contiguous 4 KiB, one block per 256 float4 (no
+// grid-stride loop).  Of the shapes probed on the box (tools/copyprobe: 1 /
+// 2 / 4 / 8 float4 per thread, block-contiguous or grid-stride, plain or
+// nontemporal) this one moves the most: 6.3-6.5 TB/s read + write over 2 GiB
+// against 4.4 TB/s for a grid-stride loop of 4 float4 per thread
+// (bench.py cosine_roofline).
 constexpr int COPY_THREADS = 256;
-constexpr int COPY_UNROLL = 4;
 
 __global__ __launch_bounds__(COPY_THREADS) void k_stream_copy(const float4* __restrict__ src,
                                                               float4* __restrict__ dst, int64_t n4) {
-  const int64_t stride = (int64_t)gridDim.x * COPY_THREADS;
-  int64_t i = (int64_t)blockIdx.x * COPY_THREADS + threadIdx.x;
-  for (; i + (COPY_UNROLL - 1) * stride < n4; i += COPY_UNROLL * stride) {
-    float4 v[COPY_UNROLL];
-#pragma unroll
-    for (int u = 0; u < COPY_UNROLL; ++u) v[u] = src[i + u * stride];
-#pragma unroll
-    for (int u = 0; u < COPY_UNROLL; ++u) dst[i + u * stride] = v[u];
-  }
-  for (; i < n4; i += stride) dst[i] = src[i];
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int64_t i = (int64_t)blockIdx.x * COPY_THREADS + threadIdx.x;
+  if (i < n4)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const v4f*>(src) + i),
+                                reinterpret_cast<v4f*>(dst) + i);
 }
 
 }  // namespace tt

@@ -1229,9 +1229,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
 // LDS: the W8 images of both towers (phases 0-3) are reused for tower 0's dU
 // image and the U / V exchange region for tower 1's, once dA1 has read W8.
 // ---------------------------------------------------------------------------
-template <int NDT>
+template <int NDT, int R_ = 64>
 struct PairLds {
-  static constexpr int R = 64;
+  static constexpr int R = R_;           // rows per block (64, or 32 for small batches)
+  static constexpr int WT = R / 16;      // waves per tower
+  static constexpr int NW = 2 * WT;      // waves per block
   static constexpr int DP = 16 * NDT;
   static constexpr int CH = DP / 4;      // 8-B chunks per dU image row
   static constexpr int LDW = H1;         // W8 image row (bf16)
@@ -1247,33 +1249,36 @@ struct PairLds {
   static constexpr int dU1 = XCi;                   // tower 1's dU image, after dA1
   static constexpr int xc_h = 2 * R * XLD * 2;      // exchange size, bf16 units
   static constexpr int hend = XCi + (xc_h > 3 * PU ? xc_h : 3 * PU);
-  static_assert(2 * 3 * PW == 3 * PU, "tower 0's dU image replaces the two W8 images");
+  static_assert(3 * PU <= 2 * 3 * PW, "tower 0's dU image inside the two W8 images");
   static_assert(A1i % 8 == 0 && XCi % 8 == 0 && hend % 8 == 0, "16-B aligned regions");
   // fp32 region (float units)
   static constexpr int b8s = hend / 2;              // [tower][DP] (0 for d >= D)
   static constexpr int cf1 = b8s + 2 * DP;          // [tower][4][H1] mean | gamma*inv | beta | inv
-  static constexpr int red = cf1 + 8 * H1;          // [8 waves][2*H1] dgamma1 | dbeta1 partials (tower = w >> 2)
-  static constexpr int scal = red + 16 * H1;        // [4 waves][2] (loss, dls) partials of the tower-0 waves
-  static constexpr int rsc = scal + 8;              // [512] replica-sum scratch
-  static constexpr int rst = rsc + 512;             // [tower][2*H1] BN1 moment sums
+  static constexpr int red = cf1 + 8 * H1;          // [NW waves][2*H1] dgamma1 | dbeta1 partials (tower = w / WT)
+  static constexpr int scal = red + NW * 2 * H1;    // [WT waves][2] (loss, dls) partials of the tower-0 waves
+  static constexpr int rsc = scal + 8;              // [8 R] replica-sum scratch
+  static constexpr int rst = rsc + 8 * R;           // [tower][2*H1] BN1 moment sums
   static constexpr int total = rst + 4 * H1;
 };
 
-template <int NDT>
-__global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a) {
-  using L = PairLds<NDT>;
-  constexpr int R = L::R, NTH = 512, DP = L::DP;
+// R = 64: both towers of 64 rows (8 waves); R = 32 (batches below the folded
+// path: twice the blocks on the same CUs) 4 waves of 16 rows
+template <int NDT, int R>
+__global__ __launch_bounds__(R * 8) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a) {
+  using L = PairLds<NDT, R>;
+  constexpr int NTH = R * 8, DP = L::DP, WT = L::WT;
   constexpr int WF4 = DP * (H1 / 4);                // float4 of one tower's padded W8
   constexpr int WPT = (2 * WF4 + NTH - 1) / NTH;    // both towers' W8: float4 per thread
   static_assert(NDT % 2 == 0, "a dA1 K step pairs two latent tiles");
   static_assert(2 * WF4 % NTH == 0, "whole W8 float4 rounds");
+  static_assert(2 * DP <= NTH && 4 * H1 <= NTH, "b8 / BN1-affine lanes");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint16_t* hs = reinterpret_cast<uint16_t*>(smem);
   const int64_t step = step_current(a);
   const int64_t r0 = (int64_t)tile64(a) * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
-  const int tw = __builtin_amdgcn_readfirstlane(w >> 2);  // this wave's tower (uniform: scalar a.tw[tw] reads)
-  const int rl = 16 * (w & 3) + r;   // this lane's row in the tile
+  const int tw = __builtin_amdgcn_readfirstlane(w / WT);  // this wave's tower (uniform: scalar a.tw[tw] reads)
+  const int rl = 16 * (w % WT) + r;  // this lane's row in the tile
   const int64_t row = r0 + rl;
   const int D = a.D;
   const TowerDev& T = a.tw[tw];
@@ -1517,25 +1522,25 @@ __global__ __launch_bounds__(512) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs a)
   // adjacent in a replica)
   if (threadIdx.x < 4 * H1) {
     const int tt = (int)threadIdx.x / (2 * H1), k = (int)threadIdx.x % (2 * H1);
-    const float v = wave_rows_sum<4>(smem + L::red + tt * 4 * 2 * H1, 2 * H1, k);
+    const float v = wave_rows_sum<WT>(smem + L::red + tt * WT * 2 * H1, 2 * H1, k);
     xblock_add(a.det, pick(tt, a.tw[0].gg1, a.tw[1].gg1), BNG, pick(tt, a.tw[0].dslot, a.tw[1].dslot), 2 * H1, k, v);
   }
   if (threadIdx.x < 2) {
     const int c = threadIdx.x;  // 0: dL/dlogit_scale, 1: batch-mean loss
-    const float v = wave_rows_sum<4>(smem + L::scal + 1 - c, 2, 0);
+    const float v = wave_rows_sum<WT>(smem + L::scal + 1 - c, 2, 0);
     xblock_add(a.det, a.lsr, LSR, a.dslot_lsr, 2, c, c == 0 ? v : v / (float)a.B);
   }
   TT_STAMP(2, 5);
 
   // ---- phase 5: dW8 (as dW8^T[h][d]) and db8 of the wave's tower over the
-  // 64 rows (K = rows, two 32-row steps); its 4 waves own latent tiles
-  // (w & 3), (w & 3) + 4, ...
+  // R rows (K = rows, 32-row steps); its WT waves own latent tiles
+  // (w % WT), (w % WT) + WT, ...
   {
     float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
     const uint16_t* dUs = hs + (tw == 0 ? L::dU0 : L::dU1);
     const uint16_t* a1b = hs + L::A1i + tw * 3 * L::PA1;
     const bf16x8 ones = __builtin_bit_cast(bf16x8, (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
-    for (int pt = w & 3; pt < NDT; pt += 4) {
+    for (int pt = w % WT; pt < NDT; pt += WT) {
       f32x4 acc[2] = {zero4(), zero4()};
       f32x4 accb = zero4();
 #pragma unroll
@@ -2374,8 +2379,10 @@ TT_L0(8)
 template __global__ void k_l0_fwd<64, 1, true, true>(StepArgs, LateRed);
 template __global__ void k_l0_fwd<64, 2, true, true>(StepArgs, LateRed);
 template __global__ void k_l4_fwd<64>(StepArgs);
-template __global__ void k_top_pair<4>(StepArgs);
-template __global__ void k_top_pair<8>(StepArgs);
+template __global__ void k_top_pair<4, 64>(StepArgs);
+template __global__ void k_top_pair<8, 64>(StepArgs);
+template __global__ void k_top_pair<4, 32>(StepArgs);
+template __global__ void k_top_pair<8, 32>(StepArgs);
 template __global__ void k_top<4, 64, false>(StepArgs);
 template __global__ void k_top<8, 64, false>(StepArgs);
 template __global__ void k_top<4, 128, false>(StepArgs);

@@ -79,6 +79,12 @@ using CfgSim = Cfg<256, 128, 64>;
 using CfgSim = Cfg<256, 256, 128>;
 #endif
 using CfgGrad = Cfg<256, 256, 128>;
+#ifndef TT_NCE_PIPE
+// the similarity kernels' gemm_loop reads B fragments one tile ahead of the
+// MFMAs (cfg 5: fwd 28.2 -> 27.9 ms, ranks 23.9 -> 23.6 ms); the gradient
+// kernels do not (their dF / dC loop measured 57.2 -> 65.8 ms with it)
+#define TT_NCE_PIPE 1
+#endif
 constexpr int TILE = 256;                                    // floats per 16x16 tile
 constexpr float SUM_MIN = 1e-30f;  // row/col sums below this: exp underflow (reported)
 
@@ -370,7 +376,7 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* L, int plane, int m, int 
 // Main loop: acc[TM][TN] += A[m0.., k-range] B[n0.., k-range]^T.  One LDS
 // stage; the next chunk's global loads are in flight during the MFMAs of the
 // current one.
-template <int SA, int SB, class C, bool LSE = false>
+template <int SA, int SB, class C, bool LSE = false, bool PIPE = false>
 __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_t n0, int64_t kb, int64_t ke,
                                           uint16_t* smem, f32x4 (&acc)[TM][C::TN]) {
   constexpr int NT = C::NTH, BM_ = C::BM, BN = C::BN, TN = C::TN, WN = C::WN;
@@ -402,6 +408,27 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int p = 0; p < NPL; ++p) a[i][p] = frag<SWZ, BM_>(As, p, wm * WM + 16 * i + r, g);
+    if constexpr (PIPE) {
+    // B fragments one tile ahead: tile j + 1's LDS reads are issued before
+    // tile j's 24 MFMAs (pinned by scheduling barriers), so their latency
+    // hides behind them instead of ahead of every tile's first MFMA
+    bf16x8 b[2][NPL];
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) b[0][p] = frag<SWZ, BN>(Bs, p, wn * WN + r, g);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j + 1 < TN) {
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) b[(j + 1) & 1][p] = frag<SWZ, BN>(Bs, p, wn * WN + 16 * (j + 1) + r, g);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = mfma_bf16(a[i][PA[q]], b[j & 1][PB[q]], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    } else {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bf16x8 b[NPL];
@@ -411,6 +438,7 @@ __device__ __forceinline__ void gemm_loop(const GemmArgs& g_, int64_t m0, int64_
       for (int q = 0; q < 6; ++q)
 #pragma unroll
         for (int i = 0; i < TM; ++i) acc[i][j] = mfma_bf16(a[i][PA[q]], b[PB[q]], acc[i][j]);
+    }
     }
   }
 }
@@ -606,7 +634,7 @@ __global__ __launch_bounds__(CfgSim::NTH) void k_nce_sim(GemmArgs a) {
 #elif TT_NCE_SIM_DB
   gemm_loop_db<C>(a, m0, n0, smem, acc);
 #else
-  gemm_loop<SRC_MK, SRC_MK, C>(a, m0, n0, 0, a.A.kdim, smem, acc);
+  gemm_loop<SRC_MK, SRC_MK, C, false, (bool)TT_NCE_PIPE>(a, m0, n0, 0, a.A.kdim, smem, acc);
 #endif
 
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;

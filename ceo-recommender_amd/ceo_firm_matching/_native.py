@@ -218,10 +218,10 @@ def set_deterministic(desc: TTModelDesc, on: bool) -> TTModelDesc:
 
 def step_plan(desc: TTModelDesc, batch: int) -> dict:
     """How one fused training step runs at this batch size (tt_step_plan)."""
-    info = (ctypes.c_int32 * 6)()
-    check(lib().tt_step_plan(ctypes.byref(desc), int(batch), info, 6), "tt_step_plan")
+    info = (ctypes.c_int32 * 8)()
+    check(lib().tt_step_plan(ctypes.byref(desc), int(batch), info, 8), "tt_step_plan")
     return {"folded_bn0_backward": bool(info[0]), "top_rows": info[1], "mid_rows": info[2], "kernels": info[3],
-            "top_pair": bool(info[4]), "ndt": info[5]}
+            "top_pair": bool(info[4]), "ndt": info[5], "fwd_rows": info[6], "train_top_rows": info[7]}
 
 
 def param_count(desc: TTModelDesc) -> int:

@@ -189,7 +189,12 @@ static std::once_flag g_attr_once;
 static void set_lds_attrs() {
   std::call_once(g_attr_once, [] {
     const int mx = (int)LDS_MAX;
-    const void* ks[] = {(const void*)k_l0_fwd<ROWS, 1, true, false>, (const void*)k_l0_fwd<ROWS, 1, false, false>,
+    const void* ks[] = {(const void*)k_l0_fwd<32, 1, true, false>, (const void*)k_l0_fwd<32, 1, false, false>,
+                        (const void*)k_l0_fwd<32, 2, true, false>, (const void*)k_l0_fwd<32, 2, false, false>,
+                        (const void*)k_l0_fwd<32, 4, true, false>, (const void*)k_l0_fwd<32, 4, false, false>,
+                        (const void*)k_l0_fwd<32, 8, true, false>, (const void*)k_l0_fwd<32, 8, false, false>,
+                        (const void*)k_l4_fwd<32>, (const void*)k_bwd_mid<32>, (const void*)k_bwd_first<32>,
+                        (const void*)k_l0_fwd<ROWS, 1, true, false>, (const void*)k_l0_fwd<ROWS, 1, false, false>,
                         (const void*)k_l0_fwd<ROWS, 2, true, false>, (const void*)k_l0_fwd<ROWS, 2, false, false>,
                         (const void*)k_l0_fwd<ROWS, 4, true, false>, (const void*)k_l0_fwd<ROWS, 4, false, false>,
                         (const void*)k_l0_fwd<ROWS, 8, true, false>, (const void*)k_l0_fwd<ROWS, 8, false, false>,
@@ -210,9 +215,12 @@ static void set_lds_attrs() {
 }
 
 struct Plan {
-  size_t lds_l0, lds_l4, lds_top, lds_mid, lds_first, lds_pair;
+  size_t lds_l0, lds_l4, lds_l4_32, lds_top, lds_mid, lds_first, lds_pair;
   bool top_pair;    // training steps run k_top_pair (both towers per block)
   int pair_rows;    // its rows per block: 64, or 32 below the folded path (twice the blocks)
+  int fwd_rows;     // k_l0_fwd / k_l4_fwd rows per block: 64, or 32 below the folded path
+  int bwd_rows;     // k_bwd_mid / k_bwd_first rows per block (unfolded): 64, or 32 below the folded path
+  int n_tiles_fwd;  // their tiles (deterministic slots of their BN moments)
   int n_tiles_pair; // its tiles (a training step's k_top slab count)
   int ndt;
   int top_rows;     // row tile of k_top (64, or 128 for large batches)
@@ -251,20 +259,24 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   // re-measured with this round's kernels: 44.1 vs 43.7 us (k_bwd_mid_fold
   // takes 14.1 us on its 64 blocks: its per-block chain, not bandwidth)
   P->fold = L.fold_ok && B >= TT_FOLD_MIN_B;
-  P->n_tiles_mid = P->fold ? (int)((P->n_tiles * ROWS) / FOLD_ROWS) : P->n_tiles;
+  P->bwd_rows = !P->fold && B < TT_BWD32_MAX_B ? 32 : ROWS;
+  P->n_tiles_mid = (int)((P->n_tiles * ROWS) / (P->fold ? FOLD_ROWS : P->bwd_rows));
   P->lds_l0 = L0Lds<ROWS>::bytes(kpm);
   P->lds_l4 = L4Lds<ROWS>::bytes;
+  P->lds_l4_32 = L4Lds<32>::bytes;
   const int tl = P->ndt == 4 ? (P->top_rows == 64 ? TopLds<4, 64>::total : TopLds<4, 128>::total)
                              : (P->top_rows == 64 ? TopLds<8, 64>::total : TopLds<8, 128>::total);
   P->lds_top = sizeof(float) * (size_t)tl;
   // below the folded path the 64-row k_top_pair leaves CUs idle (cfg 2: 64
   // blocks on 256 CUs): 32-row blocks there (TT_PAIR32_MAX_B = 0: never)
   P->pair_rows = P->top_pair && !P->fold && B < TT_PAIR32_MAX_B ? 32 : 64;
+  P->fwd_rows = !P->fold && B < TT_FWD32_MAX_B ? 32 : 64;
+  P->n_tiles_fwd = (int)((P->n_tiles * ROWS) / P->fwd_rows);
   P->n_tiles_pair = (int)((P->n_tiles * ROWS) / P->pair_rows);
   P->lds_pair = sizeof(float) * (size_t)(P->pair_rows == 32 ? (P->ndt == 4 ? PairLds<4, 32>::total : PairLds<8, 32>::total)
                                                             : (P->ndt == 4 ? PairLds<4>::total : PairLds<8>::total));
-  P->lds_mid = P->fold ? FoldLds<FOLD_ROWS>::bytes : MidLds<ROWS>::bytes;
-  P->lds_first = FirstLds<ROWS>::bytes(kpm);
+  P->lds_mid = P->fold ? FoldLds<FOLD_ROWS>::bytes : P->bwd_rows == 32 ? MidLds<32>::bytes : MidLds<ROWS>::bytes;
+  P->lds_first = P->bwd_rows == 32 ? FirstLds<32>::bytes(kpm) : FirstLds<ROWS>::bytes(kpm);
   P->lds_gen_fwd = gen_fwd_lds(d->latent);
   P->lds_gen_bwd = gen_bwd_lds(d->latent);
   if (P->top_gen) {  // 64-row top tiles (the W8 slabs of the generic backward)
@@ -455,8 +467,8 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
         r.seg[k - 1].keep = 1;  // zeroed by the next step's k_l0_fwd
     } else {
       // W0 and b0 apart: the slab's W0 range may be sized for the folded P | Q
-      add(s[TT_SLOT_W0], (int64_t)H0 * L.in_dim[t], 0, t, L.so[t][0], P.n_tiles);
-      add(s[TT_SLOT_B0], H0, 0, t, L.so[t][1], P.n_tiles);
+      add(s[TT_SLOT_W0], (int64_t)H0 * L.in_dim[t], 0, t, L.so[t][0], P.n_tiles_mid);  // k_bwd_first's tiles
+      add(s[TT_SLOT_B0], H0, 0, t, L.so[t][1], P.n_tiles_mid);
       add(s[TT_SLOT_G0], 2 * H0, 2, t, 0, 0, bng, BNG);
     }
     late_range = true;
@@ -616,14 +628,20 @@ static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = 
       launch(k_l0_fwd<ROWS, 2, true, true>, grid, blk, P.lds_l0, s, ev, a, *late);
     return;
   }
-  const dim3 grid(P.n_tiles, 2);
-#define TT_L0(KS)                                                                   \
-  if (ks == KS) {                                                                   \
-    if (vec)                                                                        \
-      launch(k_l0_fwd<ROWS, KS, true, false>, grid, blk, P.lds_l0, s, ev, a, none); \
-    else                                                                            \
-      launch(k_l0_fwd<ROWS, KS, false, false>, grid, blk, P.lds_l0, s, ev, a, none);\
-    return;                                                                         \
+  const dim3 grid(P.n_tiles_fwd, 2), blk32(4 * 32);
+#define TT_L0(KS)                                                                        \
+  if (ks == KS) {                                                                        \
+    if (P.fwd_rows == 32) {                                                              \
+      if (vec)                                                                           \
+        launch(k_l0_fwd<32, KS, true, false>, grid, blk32, P.lds_l0, s, ev, a, none);    \
+      else                                                                               \
+        launch(k_l0_fwd<32, KS, false, false>, grid, blk32, P.lds_l0, s, ev, a, none);   \
+    } else if (vec) {                                                                    \
+      launch(k_l0_fwd<ROWS, KS, true, false>, grid, blk, P.lds_l0, s, ev, a, none);      \
+    } else {                                                                             \
+      launch(k_l0_fwd<ROWS, KS, false, false>, grid, blk, P.lds_l0, s, ev, a, none);     \
+    }                                                                                    \
+    return;                                                                              \
   }
   TT_L0(1)
   TT_L0(2)
@@ -632,11 +650,17 @@ static void launch_l0(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = 
 #undef TT_L0
 }
 static void launch_l4(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
-  launch(k_l4_fwd<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_l4, s, ev, a);
+  if (P.fwd_rows == 32)
+    launch(k_l4_fwd<32>, dim3(P.n_tiles_fwd, 2), dim3(4 * 32), P.lds_l4_32, s, ev, a);
+  else
+    launch(k_l4_fwd<ROWS>, dim3(P.n_tiles_fwd, 2), dim3(4 * ROWS), P.lds_l4, s, ev, a);
 }
 static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
   if (!a.fr_zero) {
-    launch(k_bwd_mid<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_mid, s, ev, a);
+    if (P.bwd_rows == 32)
+      launch(k_bwd_mid<32>, dim3(P.n_tiles_mid, 2), dim3(4 * 32), P.lds_mid, s, ev, a);
+    else
+      launch(k_bwd_mid<ROWS>, dim3(P.n_tiles_mid, 2), dim3(4 * ROWS), P.lds_mid, s, ev, a);
     return;
   }
   const dim3 grid(P.n_tiles_mid, 2), blk(4 * FOLD_ROWS);
@@ -649,7 +673,10 @@ static void launch_mid(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev =
 // tt_step_plan tells the caller which kernels a step runs)
 static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev = {}) {
   if (a.fr_zero) return;
-  launch(k_bwd_first<ROWS>, dim3(P.n_tiles, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
+  if (P.bwd_rows == 32)
+    launch(k_bwd_first<32>, dim3(P.n_tiles_mid, 2), dim3(4 * 32), P.lds_first, s, ev, a);
+  else
+    launch(k_bwd_first<ROWS>, dim3(P.n_tiles_mid, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
 static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}, bool ex = false) {
   const dim3 grid((unsigned)(r.vn / RED_E)), blk(RED_E * RED_G);
@@ -702,14 +729,14 @@ static void det_fold(const StepArgs& a, const Plan& P, DetPoint pt, hipStream_t 
   };
   for (int t = 0; t < 2; ++t) {
     const TowerDev& T = a.tw[t];
-    if (pt == DET_L0) add(T.dslot, T.st0, P.n_tiles, 2 * H0);
-    if (pt == DET_L4) add(T.dslot, T.st1, P.n_tiles, 2 * H1);
+    if (pt == DET_L0) add(T.dslot, T.st0, P.n_tiles_fwd, 2 * H0);
+    if (pt == DET_L4) add(T.dslot, T.st1, P.n_tiles_fwd, 2 * H1);
     if (pt == DET_TOP) add(T.dslot, T.gg1, P.n_tiles_top, 2 * H1);
     if (pt == DET_MID) {
       if (P.fold)
         add(T.dslot, T.fr, P.n_tiles_mid, FRW);
       else
-        add(T.dslot, T.gg0, P.n_tiles, 2 * H0);
+        add(T.dslot, T.gg0, P.n_tiles_mid, 2 * H0);
     }
   }
   // (the generic top's embedding backward writes no (dls, loss) slots: its
@@ -807,10 +834,12 @@ int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32
   if (rc) return rc;
   info[0] = P.fold ? 1 : 0;
   info[1] = P.top_rows;
-  info[2] = P.fold ? FOLD_ROWS : ROWS;
+  info[2] = P.fold ? FOLD_ROWS : P.bwd_rows;
   info[3] = P.fold ? 5 : 6;
   if (n_info >= 5) info[4] = P.top_pair ? 1 : 0;
   if (n_info >= 6) info[5] = P.ndt;
+  if (n_info >= 7) info[6] = P.fwd_rows;
+  if (n_info >= 8) info[7] = P.top_pair ? P.pair_rows : P.top_rows;
   return TT_OK;
 }
 
@@ -876,7 +905,9 @@ int32_t tt_embed_forward(const tt_model_desc* d, const float* params, float* buf
 // eval-mode backward and input gradients need dZ0 per row, which the fold
 // never forms.
 static void unfold(Plan& P) {
+  if (!P.fold) return;  // (already the unfolded plan, possibly on 32-row tiles)
   P.fold = false;
+  P.bwd_rows = ROWS;
   P.n_tiles_mid = P.n_tiles;
   P.lds_mid = MidLds<ROWS>::bytes;
 }
@@ -1018,6 +1049,10 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
     return e;
   };
   if ((defer || pending) && !l0_late_ok(a)) return TT_ERR_UNSUPPORTED;  // (nothing enqueued yet)
+  if (defer || pending) {  // the late half rides in the 64-row k_l0_fwd: 64-row forward tiles
+    c.P.fwd_rows = ROWS;
+    c.P.n_tiles_fwd = c.P.n_tiles;
+  }
   LateRed late;
   if (pending) {  // the previous step's late half (same batch size: the caller flushes otherwise)
     RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);

@@ -91,14 +91,91 @@ __global__ __launch_bounds__(DET_COLS * DET_GROUPS) void k_det_fold(DetFold f) {
   }
 }
 
+#ifndef TT_DET_SCATTER_V2
+#define TT_DET_SCATTER_V2 0
+#endif
+#if TT_DET_SCATTER_V2
+// Embedding-table gradients in deterministic mode (model.py:69,74 backward,
+// EmbeddingBackward): block (x, y) owns 256 consecutive (code, element)
+// entries of categorical column y -- the codes c_lo .. c_hi -- and walks the
+// batch in row order.  Per chunk of DET_SCAT_CHUNK rows it stages the codes,
+// keeps the rows whose code falls in its range (a stable compaction: wave
+// ballots, waves in order), and every entry adds its code's kept rows' dX in
+// that order -- the batch-row order of the reference's sum, so every entry of
+// every table is written (codes absent from the batch get 0) and the gacc
+// arena needs no zeroing in between.  A block reads the B codes once and
+// then only its own codes' rows: table_rows x E x B compares became
+// blocks x B + B x E (large label-encoded vocabularies).
+constexpr int DET_SCAT_CHUNK = 2048;
+__global__ __launch_bounds__(256) void k_det_scatter(StepArgs a) {
+  __shared__ int codes[DET_SCAT_CHUNK];
+  __shared__ int sel_row[DET_SCAT_CHUNK];   // chunk-local row of a kept row, in row order
+  __shared__ int sel_code[DET_SCAT_CHUNK];
+  __shared__ int wcnt[4];
+  int j = (int)blockIdx.y, t = 0;
+  if (j >= a.tw[0].n_cat) {
+    j -= a.tw[0].n_cat;
+    t = 1;
+  }
+  const TowerDev& T = a.tw[t];
+  const int E = T.emb_dim, rows = T.emb_rows[j];
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x;
+  if (q0 >= (int64_t)rows * E) return;  // whole block past the table
+  const int64_t q = q0 + threadIdx.x;   // entry code * E + e
+  const int code = (int)(q / E), e = (int)(q - (int64_t)code * E);
+  const bool live = code < rows;
+  const int c_lo = (int)(q0 / E), c_hi = (int)min((q0 + (int64_t)blockDim.x - 1) / E, (int64_t)rows - 1);
+  const int64_t base = batch_row0(a, step_current(a));
+  const float* dx = T.demb + j * E + e;
+  const int w = wave_id(), l = lane_id();
+  const uint64_t below = l ? (~0ull >> (64 - l)) : 0ull;  // lanes < l
+  float acc = 0.f;
+  for (int64_t r0 = 0; r0 < a.B; r0 += DET_SCAT_CHUNK) {
+    const int n = (int)min((int64_t)DET_SCAT_CHUNK, a.B - r0);
+    __syncthreads();  // the previous chunk's lists are consumed
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      int64_t c = T.cat[data_row(a, base, r0 + i) * T.cat_ld + j];
+      codes[i] = (int)(c < 0 ? 0 : (c >= rows ? rows - 1 : c));  // the kernels' clamp
+    }
+    __syncthreads();
+    int nsel = 0;
+    for (int s0 = 0; s0 < n; s0 += 256) {
+      const int i = s0 + (int)threadIdx.x;
+      const int c = i < n ? codes[i] : -1;
+      const bool keep = c >= c_lo && c <= c_hi;
+      const uint64_t bal = __ballot(keep);
+      if (l == 0) wcnt[w] = __popcll(bal);
+      __syncthreads();
+      int woff = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        woff += k < w ? wcnt[k] : 0;
+        tot += wcnt[k];
+      }
+      if (keep) {
+        const int at = nsel + woff + __popcll(bal & below);
+        sel_row[at] = i;
+        sel_code[at] = c;
+      }
+      nsel += tot;
+      __syncthreads();  // wcnt reused; the lists complete
+    }
+    if (live)
+      for (int k = 0; k < nsel; ++k)
+        if (sel_code[k] == code) acc += dx[(r0 + sel_row[k]) * T.emb_w];
+  }
+  if (live) T.gemb[j][q] = acc;
+}
+
+#else
+constexpr int DET_SCAT_CHUNK = 2048;
 // Embedding-table gradients in deterministic mode (model.py:69,74 backward,
 // EmbeddingBackward): block (x, y) owns 256 consecutive (code, element)
 // entries of categorical column y (towers' columns concatenated); it stages
 // the batch's codes in chunks and adds the rows' dX (k_bwd_first, T.demb) in
 // batch-row order.  Every entry of every table is written (codes absent from
 // the batch get 0), so the gacc arena needs no zeroing in between.
-constexpr int DET_SCAT_CHUNK = 2048;
-__global__ __launch_bounds__(256) void k_det_scatter(StepArgs a) {
+__global__ __launch_bounds__(256) void k_det_scatter(StepArgs a) {  // (round-3 form)
   __shared__ int codes[DET_SCAT_CHUNK];
   int j = (int)blockIdx.y, t = 0;
   if (j >= a.tw[0].n_cat) {
@@ -128,6 +205,8 @@ __global__ __launch_bounds__(256) void k_det_scatter(StepArgs a) {
   }
   if (live) T.gemb[j][q] = acc;
 }
+
+#endif
 
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ P, const float* __restrict__ G,
                                               float* __restrict__ M, float* __restrict__ V, int64_t n,

@@ -382,7 +382,8 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, 
   constexpr int NTH = R * 4;
   constexpr int KC = 32 * KS, LDK = L0Lds<R>::ldk(KS), PL = H0 * LDK;
   constexpr int C4N = KC / 4, N4 = H0 * C4N, WPT = N4 / NTH;  // W0 float4 per thread
-  static_assert(R == 64 && N4 % NTH == 0, "4 waves x 16 rows");
+  constexpr int NW = R / 16, SPW = 4 / NW;  // waves; shift-row tiles per wave
+  static_assert((R == 64 || (R == 32 && !LATE)) && N4 % NTH == 0, "4 (or 2) waves x 16 rows");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if constexpr (LATE) {
     static_assert(LATE_G * RED_E == NTH, "a late-half block is one k_l0_fwd block");
@@ -397,11 +398,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, 
   const TowerDev& T = a.tw[t];
   const int64_t step = step_for_first_kernel(a);
   const int64_t base = batch_row0(a, step);
-  const int64_t r0 = (int64_t)tile64(a) * R;
+  const int64_t r0 = (int64_t)(R == 64 ? tile64(a) : (int)blockIdx.x) * R;
   const int in = T.in_dim;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   uint16_t* Wh = reinterpret_cast<uint16_t*>(smem);
-  float* red = reinterpret_cast<float*>(Wh + 3 * PL);  // [4 waves][128]
+  float* red = reinterpret_cast<float*>(Wh + 3 * PL);  // [NW waves][128]
   float* shl = red + 4 * 2 * H0;                       // [64] moment shift = Z0 of batch row 0
   TT_STAMP(0, 0);
 
@@ -430,7 +431,9 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, 
   float bias[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = T.b0[16 * j + r];
-  const float bsh = T.b0[16 * w + r];
+  float bsh[SPW];  // the shift row's tiles of this wave: w, w + NW, ...
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) bsh[i] = T.b0[16 * (w + NW * i) + r];
   // (target, weight) of this lane's row for the top kernel (tower-0 blocks
   // store them at the end): issued last, from the row index the lane already
   // holds, unconditionally (valid dummy address without a target) -- no
@@ -457,9 +460,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, 
   // column 16j + r.  Shift row: wave w computes Z0[row 0] columns 16w..16w+15
   // with the same MFMA sequence in every block (bitwise one shift for all),
   // which keeps var = S2/B - (S1/B)^2 free of cancellation for any data offset.
-  f32x4 acc[4], accs = zero4();
+  f32x4 acc[4], accs[SPW];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = zero4();
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) accs[i] = zero4();
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk) {
     zero_x8<VEC>(T, 32 * kk + 8 * g, xr[kk]);
@@ -475,19 +480,26 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, 
         wf[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * j + r) * LDK + 32 * kk + 8 * g);
       mfma_x3(xa, wf, acc[j]);
     }
-    // the shift row's tile w: its own fragment read (no per-tile branch
-    // between the MFMA chains), the same six-product sequence in every block
-    bf16x8 ws[3];
+    // the shift row's tiles w, w + NW, ...: their own fragment reads (no
+    // per-tile branch between the MFMA chains), the same six-product sequence
+    // in every block
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-      ws[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * w + r) * LDK + 32 * kk + 8 * g);
-    mfma_x3(xs, ws, accs);
+    for (int i = 0; i < SPW; ++i) {
+      bf16x8 ws[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        ws[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * (w + NW * i) + r) * LDK + 32 * kk + 8 * g);
+      mfma_x3(xs, ws, accs[i]);
+    }
   }
   if (a.train) {
     if (g == 0) {
-      const float sh = accs[0] + bsh;
-      shl[16 * w + r] = sh;
-      if (blockIdx.x == 0) T.shift0[16 * w + r] = sh;
+#pragma unroll
+      for (int i = 0; i < SPW; ++i) {
+        const float sh = accs[i][0] + bsh[i];
+        shl[16 * (w + NW * i) + r] = sh;
+        if (blockIdx.x == 0) T.shift0[16 * (w + NW * i) + r] = sh;
+      }
     }
     __syncthreads();  // shl
   }
@@ -532,13 +544,14 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, 
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H0)
-      xblock_add(a.det, T.st0, 2 * H0, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<4>(red, 2 * H0, threadIdx.x));
+      xblock_add(a.det, T.st0, 2 * H0, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<NW>(red, 2 * H0, threadIdx.x));
   }
   // the folded BN0 backward's replicas start every step at zero (k_bwd_mid
   // accumulates them, k_reduce_adam only reads them)
-  if (a.fr_zero) {  // (the row-tile blocks only: l0_gx, not gridDim.x)
-    const int nthr = a.l0_gx * (int)gridDim.y * NTH;
-    for (int i = (int)((blockIdx.y * a.l0_gx + blockIdx.x) * NTH + threadIdx.x); i < a.fr_zero_len; i += nthr)
+  if (a.fr_zero) {  // (the row-tile blocks only: with LATE l0_gx, not gridDim.x)
+    const int gx = LATE ? a.l0_gx : (int)gridDim.x;
+    const int nthr = gx * (int)gridDim.y * NTH;
+    for (int i = (int)((blockIdx.y * gx + blockIdx.x) * NTH + threadIdx.x); i < a.fr_zero_len; i += nthr)
       a.fr_zero[i] = 0.f;
   }
   TT_STAMP(0, 3);
@@ -574,13 +587,13 @@ struct L4Lds {
 template <int R>
 __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) {
   using L = L4Lds<R>;
-  constexpr int NTH = R * 4, LDK = L::LDK, PL = L::PL;
-  static_assert(R == 64 && NTH == 256 && H0 == 64 && H1 == 32, "4 waves x 16 rows, two 32-deep K steps");
+  constexpr int NTH = R * 4, LDK = L::LDK, PL = L::PL, NW = R / 16;
+  static_assert((R == 64 || R == 32) && H0 == 64 && H1 == 32, "4 (or 2) waves x 16 rows, two 32-deep K steps");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
   const TowerDev& T = a.tw[t];
   const int64_t step = step_current(a);
-  const int64_t r0 = (int64_t)tile64(a) * R;
+  const int64_t r0 = (int64_t)(R == 64 ? tile64(a) : (int)blockIdx.x) * R;
   const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
   uint16_t* Wh = reinterpret_cast<uint16_t*>(smem);  // W4 planes
   float* cf = smem + L::f_cf;                        // mean[64] alpha[64] beta[64]
@@ -604,10 +617,14 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   const float z0r = threadIdx.x < H0 ? z0r_raw : 0.f;
   // W4 (raw) and wave 0's BN0 parameters are issued with the Z0 loads: one
   // round trip for the whole phase
-  static_assert(H1 * H0 / 4 == 2 * NTH, "W4: 2 float4 per thread; BN0: wave 0");
-  const int we0 = (int)threadIdx.x, we1 = (int)threadIdx.x + NTH;  // two float4 per thread (named: no array)
-  const float4 w4a = *reinterpret_cast<const float4*>(T.W4 + (we0 >> 4) * H0 + 4 * (we0 & 15));
-  const float4 w4b = *reinterpret_cast<const float4*>(T.W4 + (we1 >> 4) * H0 + 4 * (we1 & 15));
+  constexpr int W4T = H1 * H0 / 4 / NTH;  // W4 float4 per thread (2, or 4 at 32 rows); BN0: wave 0
+  static_assert(H1 * H0 / 4 == W4T * NTH, "whole W4 float4 rounds");
+  float4 w4v[W4T];
+#pragma unroll
+  for (int k = 0; k < W4T; ++k) {
+    const int we = (int)threadIdx.x + k * NTH;
+    w4v[k] = *reinterpret_cast<const float4*>(T.W4 + (we >> 4) * H0 + 4 * (we & 15));
+  }
   // (every wave loads them -- wave 0 uses them: a load under a branch would
   // make hipcc drain vmcnt at the join, i.e. wait for the whole phase here)
   const float* rmp = T.rm0 ? T.rm0 : T.g0;  // running stats NULL without buffers (never read then)
@@ -634,8 +651,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     if (a.train)
       a0r[c] = bn_relu_drop(z0r, mean, alpha, bn_be, drop, dropout_row_key(key, 0), c, a.drop_thr, a.drop_scale);
   }
-  put_planes4(Wh + (we0 >> 4) * LDK + 4 * (we0 & 15), PL, w4a);
-  put_planes4(Wh + (we1 >> 4) * LDK + 4 * (we1 & 15), PL, w4b);
+#pragma unroll
+  for (int k = 0; k < W4T; ++k) {
+    const int we = (int)threadIdx.x + k * NTH;
+    put_planes4(Wh + (we >> 4) * LDK + 4 * (we & 15), PL, w4v[k]);
+  }
   __syncthreads();
   TT_STAMP(1, 1);
 
@@ -748,7 +768,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H1)
-      xblock_add(a.det, T.st1, 2 * H1, T.dslot, 2 * H1, threadIdx.x, wave_rows_sum<4>(red, 2 * H1, threadIdx.x));
+      xblock_add(a.det, T.st1, 2 * H1, T.dslot, 2 * H1, threadIdx.x, wave_rows_sum<NW>(red, 2 * H1, threadIdx.x));
   }
   TT_STAMP(1, 4);
 }
@@ -1590,8 +1610,8 @@ struct MidLds {
 
 template <int R>
 __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
-  static_assert(R == 64, "dW4 tile ownership assumes 4 waves");
-  constexpr int NTH = R * 4;
+  static_assert(R == 64 || R == 32, "4 (or 2) waves of 16 rows");
+  constexpr int NTH = R * 4, NW = R / 16, TPW = 8 / NW;  // dW4 tiles (of 2 x 4) per wave
   constexpr int LDW = MidLds<R>::LDW, LDT = MidLds<R>::LDT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
@@ -1626,10 +1646,14 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   // W4 and the BN coefficients' inputs are issued with the tiles above (one
   // round trip; they used to follow the replica sum, W4 in two dependent
   // load -> store pairs).  Every thread loads (clamped columns): no branch.
-  static_assert(H1 * H0 / 4 == 2 * NTH, "W4: 2 float4 per thread");
-  const int we0 = (int)threadIdx.x, we1 = (int)threadIdx.x + NTH;
-  const float4 w4a = *reinterpret_cast<const float4*>(T.W4 + (we0 >> 4) * H0 + 4 * (we0 & 15));
-  const float4 w4b = *reinterpret_cast<const float4*>(T.W4 + (we1 >> 4) * H0 + 4 * (we1 & 15));
+  constexpr int W4T = H1 * H0 / 4 / NTH;  // W4 float4 per thread
+  static_assert(H1 * H0 / 4 == W4T * NTH, "whole W4 float4 rounds");
+  float4 w4v[W4T];
+#pragma unroll
+  for (int k = 0; k < W4T; ++k) {
+    const int we = (int)threadIdx.x + k * NTH;
+    w4v[k] = *reinterpret_cast<const float4*>(T.W4 + (we >> 4) * H0 + 4 * (we & 15));
+  }
   const int c1i = min((int)threadIdx.x, H1 - 1), c0i = min(max((int)threadIdx.x - H1, 0), H0 - 1);
   const float f1inv = T.fin1[H1 + c1i], f1mean = T.fin1[c1i], g1v = T.g1[c1i];
   const float f0inv = T.fin0[H0 + c0i], f0mean = T.fin0[c0i], g0v = T.g0[c0i], be0v = T.be0[c0i];
@@ -1649,8 +1673,11 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
     c0[2 * H0 + c] = be0v;
     c0[3 * H0 + c] = f0inv;
   }
-  *reinterpret_cast<float4*>(W4s + (we0 >> 4) * LDW + 4 * (we0 & 15)) = w4a;
-  *reinterpret_cast<float4*>(W4s + (we1 >> 4) * LDW + 4 * (we1 & 15)) = w4b;
+#pragma unroll
+  for (int k = 0; k < W4T; ++k) {
+    const int we = (int)threadIdx.x + k * NTH;
+    *reinterpret_cast<float4*>(W4s + (we >> 4) * LDW + 4 * (we & 15)) = w4v[k];
+  }
   __syncthreads();
   TT_STAMP(3, 1);
 
@@ -1696,14 +1723,16 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   TT_STAMP(3, 2);
 
   // dW4 = dZ4^T A0 over the tile's rows: wave w owns h1-tile (w&1) x h0-tiles
-  // 2*(w>>1)..+1 and writes them straight into this tile's slab
+  // TPW*(w>>1)..+TPW-1 and writes them straight into this tile's slab
   float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
   {
-    const int p = w & 1, q0 = 2 * (w >> 1);
-    f32x4 acc[2] = {zero4(), zero4()};
-    strip_gemm_nt<2>(dZT + 16 * p * LDT, LDT, A0T + 16 * q0 * LDT, LDT, R, acc);
+    const int p = w & 1, q0 = TPW * (w >> 1);
+    f32x4 acc[TPW];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) store_tile_rm_wt(slab, (int)T.so_W4 + 16 * p * H0 + 16 * (q0 + q), H0, acc[q]);
+    for (int q = 0; q < TPW; ++q) acc[q] = zero4();
+    strip_gemm_nt<TPW>(dZT + 16 * p * LDT, LDT, A0T + 16 * q0 * LDT, LDT, R, acc);
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) store_tile_rm_wt(slab, (int)T.so_W4 + 16 * p * H0 + 16 * (q0 + q), H0, acc[q]);
   }
 
   // dA0 = dZ4 W4  (K = 32; A from the transposed image, W4 row-major)
@@ -1730,8 +1759,8 @@ __global__ __launch_bounds__(R * 4) void k_bwd_mid(StepArgs a) {
   __syncthreads();
   TT_STAMP(3, 3);
   if (threadIdx.x < 2 * H0)  // gamma0 | beta0 grads (adjacent in a replica)
-    xblock_add(a.det, T.gg0, BNG, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<4>(red, 2 * H0, threadIdx.x));
-  if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = wave_rows_sum<4>(db4, H1, threadIdx.x);
+    xblock_add(a.det, T.gg0, BNG, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<NW>(red, 2 * H0, threadIdx.x));
+  if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = wave_rows_sum<NW>(db4, H1, threadIdx.x);
   TT_STAMP(3, 4);
 }
 
@@ -2160,8 +2189,8 @@ struct FirstLds {
 
 template <int R>
 __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
-  static_assert(R == 64, "dW0 tile ownership assumes 4 waves (one per 16 outputs of 64)");
-  constexpr int NTH = R * 4;
+  static_assert(R == 64 || R == 32, "4 (or 2) waves of 16 rows");
+  constexpr int NTH = R * 4, NW = R / 16;
   constexpr int LDT = FirstLds<R>::LDT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = blockIdx.y;
@@ -2300,11 +2329,12 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
   float* slab = T.slab + (int64_t)blockIdx.x * a.slab_ld;
   const int in = T.in_dim;
   const bool w0_vec = (in & 3) == 0 && (T.so_W0 & 3) == 0;
-  auto put_w0 = [&](int kt, const f32x4& acc) {
+  // wave w owns outputs 16 wo .. 16 wo + 15 for wo = w, w + NW, ...
+  auto put_w0 = [&](int wo, int kt, const f32x4& acc) {
     const int k = 16 * kt + r;
-    float* dst = slab + T.so_W0 + (16 * w + 4 * g) * in + k;
+    float* dst = slab + T.so_W0 + (16 * wo + 4 * g) * in + k;
     if (w0_vec && 16 * kt + 16 <= in) {  // whole tile: row-major 16-B write-through stores
-      store_tile_rm_wt(slab, (int)T.so_W0 + 16 * w * in + 16 * kt, in, acc);
+      store_tile_rm_wt(slab, (int)T.so_W0 + 16 * wo * in + 16 * kt, in, acc);
     } else if (16 * kt + 16 <= in) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) dst[i * in] = acc[i];
@@ -2313,17 +2343,20 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
       for (int i = 0; i < 4; ++i) dst[i * in] = acc[i];
     }
   };
-  int kt = 0;
-  for (; kt + 4 <= KT; kt += 4) {
-    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-    strip_gemm_nt<4>(dZT + 16 * w * LDT, LDT, XT + 16 * kt * LDT, LDT, R, acc);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) put_w0(kt + q, acc[q]);
-  }
-  for (; kt < KT; ++kt) {
-    f32x4 acc[1] = {zero4()};
-    strip_gemm_nt<1>(dZT + 16 * w * LDT, LDT, XT + 16 * kt * LDT, LDT, R, acc);
-    put_w0(kt, acc[0]);
+  for (int wo = w; wo < 4; wo += NW) {
+    int kt = 0;
+    for (; kt + 4 <= KT; kt += 4) {
+      f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+      strip_gemm_nt<4>(dZT + 16 * wo * LDT, LDT, XT + 16 * kt * LDT, LDT, R, acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) put_w0(wo, kt + q, acc[q]);
+    }
+    for (; kt < KT; ++kt) {
+      f32x4 acc[1] = {zero4()};
+      strip_gemm_nt<1>(dZT + 16 * wo * LDT, LDT, XT + 16 * kt * LDT, LDT, R, acc);
+      put_w0(wo, kt, acc[0]);
+    }
   }
   float* dxn = T.dxn;
   if (emb || dxn) {
@@ -2365,7 +2398,7 @@ __global__ __launch_bounds__(R * 4) void k_bwd_first(StepArgs a) {
       }
     }
   }
-  if (threadIdx.x < H0) slab[T.so_b0 + threadIdx.x] = wave_rows_sum<4>(db0, H0, threadIdx.x);
+  if (threadIdx.x < H0) slab[T.so_b0 + threadIdx.x] = wave_rows_sum<NW>(db0, H0, threadIdx.x);
   TT_STAMP(4, 3);
 }
 
@@ -2376,9 +2409,17 @@ TT_L0(2)
 TT_L0(4)
 TT_L0(8)
 #undef TT_L0
+#define TT_L0(KS) template __global__ void k_l0_fwd<32, KS, true, false>(StepArgs, LateRed); \
+  template __global__ void k_l0_fwd<32, KS, false, false>(StepArgs, LateRed);
+TT_L0(1)
+TT_L0(2)
+TT_L0(4)
+TT_L0(8)
+#undef TT_L0
 template __global__ void k_l0_fwd<64, 1, true, true>(StepArgs, LateRed);
 template __global__ void k_l0_fwd<64, 2, true, true>(StepArgs, LateRed);
 template __global__ void k_l4_fwd<64>(StepArgs);
+template __global__ void k_l4_fwd<32>(StepArgs);
 template __global__ void k_top_pair<4, 64>(StepArgs);
 template __global__ void k_top_pair<8, 64>(StepArgs);
 template __global__ void k_top_pair<4, 32>(StepArgs);
@@ -2392,8 +2433,10 @@ template __global__ void k_top<8, 64, true>(StepArgs);
 template __global__ void k_top<4, 128, true>(StepArgs);
 template __global__ void k_top<8, 128, true>(StepArgs);
 template __global__ void k_bwd_mid<64>(StepArgs);
+template __global__ void k_bwd_mid<32>(StepArgs);
 template __global__ void k_bwd_mid_fold<128, true>(StepArgs);
 template __global__ void k_bwd_mid_fold<128, false>(StepArgs);
 template __global__ void k_bwd_first<64>(StepArgs);
+template __global__ void k_bwd_first<32>(StepArgs);
 
 }  // namespace tt

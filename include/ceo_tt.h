@@ -151,13 +151,18 @@ int32_t tt_param_offsets(const tt_model_desc* d, int64_t* out /* TT_NUM_OFFSETS 
 /* How a training step of this model at this batch size runs (no GPU work):
  * info[0] = 1 when the BN0 backward is folded into k_bwd_mid (numeric-only
  * towers, widths % 4 == 0 and <= 64: k_bwd_first is not launched),
- * info[1] = k_top row tile, info[2] = k_bwd_mid row tile, info[3] = kernels
- * per tt_train_step (5 or 6; the event slots of tt_train_step_ev are fixed:
- * l0, l4, top, mid, first, reduce -- slot 4 stays unrecorded when folded),
+ * info[1] = k_top row tile, info[2] = k_bwd_mid (and k_bwd_first) row tile,
+ * info[3] = kernels per tt_train_step (5 or 6; the event slots of
+ * tt_train_step_ev are fixed: l0, l4, top, mid, first, reduce -- slot 4
+ * stays unrecorded when folded),
  * info[4] (n_info >= 5) = 1 when the step's k_top is k_top_pair (both
- * towers' backward per 64-row block; from B = 4096),
+ * towers' backward per block; from B = 4096),
  * info[5] (n_info >= 6) = latent tiles of 16 the top kernels are
- * instantiated for (4: LATENT <= 64, 8: LATENT <= 128).
+ * instantiated for (4: LATENT <= 64, 8: LATENT <= 128),
+ * info[6] (n_info >= 7) = k_l0_fwd / k_l4_fwd row tile,
+ * info[7] (n_info >= 8) = the training step's top row tile (k_top_pair's
+ * when info[4]).  Below the folded path (B < 8192) the tower kernels run
+ * 32-row tiles: twice the blocks of a batch that leaves CUs idle at 64.
  * Replaces nothing in the reference (training.py:44-57 is one autograd
  * pass); a query for callers that time or trace the step.             */
 int32_t tt_step_plan(const tt_model_desc* d, int64_t batch, int32_t* info, int32_t n_info);

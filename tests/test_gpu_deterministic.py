@@ -144,3 +144,48 @@ def test_deterministic_module_backward_is_repeatable():
         assert np.array_equal(g0[n], g1[n]), n
     for n in b0:
         assert np.array_equal(b0[n], b1[n]), n
+
+
+def test_deterministic_embedding_gradients_large_vocabulary():
+    """Deterministic mode with a label-encoded vocabulary of 5,000 codes
+    (k_det_scatter: each block keeps only its own codes' rows): the step's
+    embedding-table gradients -- every entry, codes absent from the batch
+    included -- vs the fp64 oracle at the parity bar, and bitwise repeatable
+    (model.py:69,74 EmbeddingBackward)."""
+    from ceo_firm_matching import CEOFirmMatcher
+    from ceo_firm_matching.engine import FusedTrainer
+    from oracle import two_tower as O
+    meta = {"n_firm_numeric": 8, "firm_cat_counts": [5000, 7], "n_ceo_numeric": 4, "ceo_cat_counts": [300]}
+    B = 1024
+    torch.manual_seed(3)
+    m0 = CEOFirmMatcher(meta, _cfg(32, 0.0))
+    sd0 = {k: v.clone() for k, v in m0.state_dict().items()}
+    P = {k: sd0[k].double() for k in O.param_names(meta)}
+    buf = {k: (sd0[k] if "num_batches" in k else sd0[k].double()) for k in O.buffer_names()}
+    for data_seed in range(7, 7 + 32):
+        bc = _data(meta, B, data_seed)
+        score, cache, _ = O.forward(P, buf, bc, train=True)
+        if all(int((c[f"y{li}"].abs() < 5e-7).sum()) == 0 for c in cache["towers"] for li in (0, 1)):
+            break
+    else:
+        raise AssertionError("no kink-free batch")
+    _, dscore = O.weighted_mse(score, bc["target"], bc["weights"])
+    grads = O.backward(P, cache, dscore)
+    outs = []
+    for _ in range(2):
+        m = CEOFirmMatcher(meta, _cfg(32, 0.0))
+        m.load_state_dict(sd0)
+        m = m.to(_dev())
+        tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=5, deterministic=True)
+        tr.set_data({k: v.to(_dev()) for k, v in bc.items()})
+        tr.step(None, 0, B)
+        torch.cuda.synchronize()
+        outs.append(tr.grad.detach().cpu().numpy().copy())
+        base = tr.arena.params.data_ptr()
+        for n, prm in m.named_parameters():
+            if "embeddings" not in n:
+                continue
+            off = (prm.data_ptr() - base) // 4
+            gk = outs[-1][off:off + prm.numel()].reshape(prm.shape)
+            assert normwise(gk, grads[n].numpy()) < TOL, (n, normwise(gk, grads[n].numpy()))
+    assert np.array_equal(outs[0], outs[1])

@@ -108,6 +108,25 @@ def test_workspace_bytes_grow_with_batch():
         N.workspace_bytes(desc, 0)
 
 
+def test_step_plan_tiles():
+    """tt_step_plan (host only): the folded five-kernel step from B = 8192,
+    k_top_pair from B = 4096 on 32-row blocks below the folded path, and the
+    other tower kernels' row tiles (32 below the folded path when the build
+    enables it: TT_FWD32_MAX_B / TT_BWD32_MAX_B)."""
+    desc = _model("cfg3").tt_desc()
+    big = N.step_plan(desc, 16384)
+    assert big["folded_bn0_backward"] and big["kernels"] == 5 and big["mid_rows"] == 128
+    assert big["top_pair"] and big["train_top_rows"] == 64 and big["fwd_rows"] == 64
+    mid = N.step_plan(desc, 6000)
+    assert not mid["folded_bn0_backward"] and mid["kernels"] == 6
+    assert mid["top_pair"] and mid["train_top_rows"] == 32
+    assert mid["fwd_rows"] in (32, 64) and mid["mid_rows"] in (32, 64)
+    small = N.step_plan(desc, 1000)
+    assert not small["top_pair"] and small["train_top_rows"] == small["top_rows"] == 64
+    # the workspace covers the doubled tile count of the 32-row kernels
+    assert N.workspace_bytes(desc, 8191) >= N.workspace_bytes(desc, 4096)
+
+
 def _fake(n=1 << 20):
     """A host buffer standing in for device pointers: argument errors are
     decided before anything dereferences or enqueues."""

@@ -34,10 +34,10 @@ constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 #define TT_PAIR32_MAX_B 8192  // training batches below it (and unfolded) run k_top_pair on 32-row blocks
 #endif
 #ifndef TT_FWD32_MAX_B
-#define TT_FWD32_MAX_B 0  // batches below it (and unfolded) run k_l0_fwd / k_l4_fwd on 32-row blocks
+#define TT_FWD32_MAX_B 0  // (off: measured slower) batches below it run k_l0_fwd / k_l4_fwd on 32-row blocks
 #endif
 #ifndef TT_BWD32_MAX_B
-#define TT_BWD32_MAX_B 0  // unfolded batches below it run k_bwd_mid / k_bwd_first on 32-row blocks
+#define TT_BWD32_MAX_B 0  // (off: measured slower) unfolded batches below it run k_bwd_mid / k_bwd_first on 32-row blocks
 #endif
 #ifndef TT_FOLD_MIN_B
 #define TT_FOLD_MIN_B 8192  // smallest batch that runs the folded BN0 backward

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(DET_COLS * DET_GROUPS) void k_det_fold(DetFold f) {
 }
 
 #ifndef TT_DET_SCATTER_V2
-#define TT_DET_SCATTER_V2 0
+#define TT_DET_SCATTER_V2 1
 #endif
 #if TT_DET_SCATTER_V2
 // Embedding-table gradients in deterministic mode (model.py:69,74 backward,

@@ -269,7 +269,10 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   P->lds_top = sizeof(float) * (size_t)tl;
   // below the folded path the 64-row k_top_pair leaves CUs idle (cfg 2: 64
   // blocks on 256 CUs): 32-row blocks there (TT_PAIR32_MAX_B = 0: never)
-  P->pair_rows = P->top_pair && !P->fold && B < TT_PAIR32_MAX_B ? 32 : 64;
+#ifndef TT_PAIR32_FOLD
+#define TT_PAIR32_FOLD 0  // probe (measured slower at cfg 3): 32-row k_top_pair on the folded path too
+#endif
+  P->pair_rows = P->top_pair && (!P->fold || TT_PAIR32_FOLD) && B < TT_PAIR32_MAX_B ? 32 : 64;
   P->fwd_rows = !P->fold && B < TT_FWD32_MAX_B ? 32 : 64;
   P->n_tiles_fwd = (int)((P->n_tiles * ROWS) / P->fwd_rows);
   P->n_tiles_pair = (int)((P->n_tiles * ROWS) / P->pair_rows);

@@ -72,8 +72,20 @@ def bound_error(got, lo, hi, ref) -> float:
     return num / den if den > 0 else num
 
 
-def adam1_bounds(O, P, lo: Dict[str, torch.Tensor], hi: Dict[str, torch.Tensor], lr: float):
-    """Parameter bounds after ONE Adam step (fresh moments: monotone in g)."""
+def adam1_bounds(O, P, lo: Dict[str, torch.Tensor], hi: Dict[str, torch.Tensor], lr: float,
+                 ref: Dict[str, torch.Tensor] = None, slack: float = 0.0):
+    """Parameter bounds after ONE Adam step (fresh moments: monotone in g).
+
+    With ``ref`` the gradient box is first widened by ``slack * max |ref|``
+    per tensor -- the band the gradient check itself accepts (bound_error <
+    slack).  The first Adam step is g / (|g| + eps): a component within that
+    band of 0 may move the parameter by anything up to +-lr (its fp32 sum's
+    order, atomic or not, picks the side), which the widened box covers; a
+    wrong update (step size, moments, bias correction) still falls outside."""
+    if ref is not None:
+        pad = {k: slack * float(ref[k].abs().max()) if ref[k].numel() else 0.0 for k in lo}
+        lo = {k: v - pad[k] for k, v in lo.items()}
+        hi = {k: v + pad[k] for k, v in hi.items()}
     outs = []
     for g in (lo, hi):
         Pc = {k: v.clone() for k, v in P.items()}

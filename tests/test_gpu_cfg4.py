@@ -118,7 +118,7 @@ def _oracle_bounds():
     avg = {k: v / WORLD for k, v in gsum.items()}
     lo = {k: v / WORLD for k, v in lsum.items()}
     hi = {k: v / WORLD for k, v in hsum.items()}
-    plo, phi = adam1_bounds(O, P, lo, hi, 4e-4)
+    plo, phi = adam1_bounds(O, P, lo, hi, 4e-4, ref=avg, slack=TOL)
     return meta, avg, lo, hi, plo, phi, losses, n_kinks
 
 

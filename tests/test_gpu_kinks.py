@@ -134,7 +134,7 @@ def test_exact_kink_zero_variance_columns(B, p, det):
     assert not np.any(_grad_of(m, tr, "firm_tower.0.weight")[5])
     assert not np.any(_grad_of(m, tr, "ceo_tower.4.weight")[7])
     # parameters after Adam, BN buffers (running_var of a constant column: 0.9 * rv + 0.1 * 0)
-    plo, phi = adam1_bounds(O, P, lo, hi, 4e-4)
+    plo, phi = adam1_bounds(O, P, lo, hi, 4e-4, ref=grads, slack=TOL)
     sd = m.state_dict()
     for n in P:
         if excluded_param(n):
@@ -180,7 +180,7 @@ def test_unscreened_large_batch_vs_kink_bounds(p, det):
         worst[n] = bound_error(_grad_of(m, tr, n), lo[n].numpy(), hi[n].numpy(), grads[n].numpy())
     bad = {k: v for k, v in worst.items() if v >= TOL}
     assert not bad, (len(elems), bad)
-    plo, phi = adam1_bounds(O, P, lo, hi, 4e-4)
+    plo, phi = adam1_bounds(O, P, lo, hi, 4e-4, ref=grads, slack=TOL)
     sd = m.state_dict()
     for n in P:
         if excluded_param(n):

@@ -30,6 +30,10 @@ constexpr int BNG = 2 * H0 + 2 * H1;  // one replica of a tower's BN-affine grad
 constexpr int FRW = 3 * H0 + 64;
 constexpr int FOLD_MAX_KP = 64;
 constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
+// k_reduce_adam's element space heaviest range first (make_red)
+#ifndef TT_RED_HEAVY_FIRST
+#define TT_RED_HEAVY_FIRST 1
+#endif
 #ifndef TT_PAIR32_MAX_B
 #define TT_PAIR32_MAX_B 8192  // training batches below it (and unfolded) run k_top_pair on 32-row blocks
 #endif

@@ -81,6 +81,13 @@ def main():
                   f"max={d.max():7.2f}")
         life = s[:, nslots - 1] - s[:, 0]
         print(f"    block life: p50={np.median(life):7.2f} max={life.max():7.2f}")
+        if os.environ.get("STAMPS_BLOCKS") and name == "k_reduce_adam":
+            # block life / end time by block index (element-space order of make_red)
+            idx = np.nonzero(m)[0]
+            for lo in range(0, len(idx), 16):
+                sl = slice(lo, lo + 16)
+                print(f"      blocks {idx[sl][0]:4d}-{idx[sl][-1]:4d}: life p50={np.median(life[sl]):5.2f} "
+                      f"max={life[sl].max():5.2f} end max={(s[sl, nslots - 1] - t0).max():5.2f}")
 
 
 if __name__ == "__main__":

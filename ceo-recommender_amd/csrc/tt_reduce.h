@@ -279,6 +279,7 @@ __device__ __forceinline__ void reduce_body(const A& a, int bid, float* part, fl
     a.p[e] = pp;
     a.m[e] = pm;
     a.v[e] = pv;
+    if constexpr (!LATE) TT_STAMP(5, 2);
     if (!LATE && a.state && bid == 0 && el == 0) a.state->step_done = t;
     if constexpr (PRE) {  // a light block caches the next step's coefficients (AdamSlot)
       if (si == a.next_seg && vb == S.voff && el == 0)

@@ -86,8 +86,9 @@ def main():
             idx = np.nonzero(m)[0]
             for lo in range(0, len(idx), 16):
                 sl = slice(lo, lo + 16)
+                ph = " ".join(f"ph{j - 1}={np.median(s[sl, j] - s[sl, j - 1]):5.2f}" for j in range(1, nslots))
                 print(f"      blocks {idx[sl][0]:4d}-{idx[sl][-1]:4d}: life p50={np.median(life[sl]):5.2f} "
-                      f"max={life[sl].max():5.2f} end max={(s[sl, nslots - 1] - t0).max():5.2f}")
+                      f"max={life[sl].max():5.2f} end max={(s[sl, nslots - 1] - t0).max():5.2f}  {ph}")
 
 
 if __name__ == "__main__":

@@ -319,6 +319,63 @@ def side_config_leg(dev, name, steps=200, warmup=20):
     return out
 
 
+def train_entry_leg(dev, name, timed_epochs=2):
+    """The north-star entry point itself: ``training.train_model`` (alias
+    ``train``, reference training.py:36-57) on a ``CEOFirmDataset`` behind a
+    ``DataLoader(shuffle=True)`` of the headline config -- model build, the
+    loader's exact batch order (the sampler's torch.randperm, built on worker
+    threads), hipGraph-replayed fused steps, the reference's prints.  Steady
+    rate = (T(1 + k epochs) - T(1 epoch)) / k epochs after one warm call: the
+    per-call setup (model, upload of the dataset to HBM, trainer) cancels."""
+    import contextlib
+    from torch.utils.data import DataLoader
+    from ceo_firm_matching import Config, training
+    from ceo_firm_matching.data import CEOFirmDataset
+    from ceo_firm_matching.engine import DATA_KEYS
+    from ceo_firm_matching.synthetic import generate_pairs
+    n_total, nf, nc, D, B = CONFIGS[name]
+    d = generate_pairs(n_total, nf, nc, seed=3, device=dev)
+    meta = {k: d[k] for k in ("n_firm_numeric", "firm_cat_counts", "n_ceo_numeric", "ceo_cat_counts")}
+    ds = CEOFirmDataset({k: d[k].cpu() for k in DATA_KEYS})  # a user's dataset: host tensors
+    del d
+    torch.cuda.empty_cache()
+    cfg = Config()
+    cfg.LATENT_DIM = D
+    cfg.DEVICE = dev
+
+    def run(epochs):
+        cfg.EPOCHS = epochs
+        torch.manual_seed(0)
+        loader = DataLoader(ds, batch_size=B, shuffle=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(sys.stderr):  # the reference's prints
+            m = training.train_model(loader, None, meta, cfg)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        del m
+        return t
+    run(1)
+    t1 = run(1)
+    tk = run(1 + timed_epochs)
+    per_epoch = (tk - t1) / timed_epochs
+    # one epoch's batch order on one host thread (the RandomSampler's
+    # torch.randperm: sequential), the work train_model's order threads overlap
+    g = torch.Generator()
+    g.manual_seed(1)
+    t0 = time.perf_counter()
+    torch.randperm(n_total, generator=g)
+    t_perm = time.perf_counter() - t0
+    steps = -(-n_total // B)
+    return {"workload": f"{name}: train_model(DataLoader(CEOFirmDataset, batch_size={B}, shuffle=True)), "
+                        f"{n_total} pairs, 1 GPU",
+            "train_entry_pairs_per_s": round(n_total / per_epoch, 1), "ms_per_epoch": round(1e3 * per_epoch, 2),
+            "us_per_step": round(1e6 * per_epoch / steps, 2), "steps_per_epoch": steps,
+            "timed_epochs": timed_epochs, "setup_plus_first_epoch_s": round(t1, 3),
+            "host_permutation_ms_per_epoch_one_thread": round(1e3 * t_perm, 2),
+            "order_threads": training._order_ahead()}
+
+
 def contrastive_cpu(D=256, B=4096):
     """CPU oracle InfoNCE fwd+bwd (the reference's info_nce_loss algebra) at
     B=4096, extrapolated to N x N pairs (work grows as B^2)."""
@@ -491,6 +548,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip roofline / cosine legs")
     ap.add_argument("--no-contrastive", action="store_true", help="skip the cfg-5 contrastive leg")
+    ap.add_argument("--no-train-entry", action="store_true",
+                    help="skip the training.train_model (DataLoader entry point) leg")
     ap.add_argument("--no-side-config", action="store_true",
                     help="skip the other single-GPU config (PMC passes: counters of the headline config only)")
     ap.add_argument("--dp", action="store_true",
@@ -608,12 +667,16 @@ def main():
     if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    region = N.trace_range(f"bench timed region: {args.steps} steps, rank {rank}")  # roctx
     t0 = time.perf_counter()
+    region.__enter__()
     if graph is not None:  # exactly K steps: K // chunk full chunks + the remainder graph
         for _ in range(args.steps // chunk):
-            graph.replay()
+            with N.trace_range(f"step chunk x{chunk}"):
+                graph.replay()
         if graph_rem is not None:
-            graph_rem.replay()
+            with N.trace_range(f"step chunk x{args.steps % chunk}"):
+                graph_rem.replay()
     elif c_steps:  # exactly K steps launched by one tt_train_steps call
         tr.step_cycle_n(rows, B, n_batches, args.steps)
     else:
@@ -626,6 +689,7 @@ def main():
     if pg is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    region.__exit__(None, None, None)
     if pg is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -679,7 +743,10 @@ def main():
                                      else "peer-memory one-shot + fused Adam" if getattr(tr, "peer", None) is not None
                                      else ("rccl all-reduce" if pg is not None and dist.get_backend(pg) == "nccl"
                                            else ("gloo all-reduce" if pg is not None else "none"))),
-                   "exchange_vs_collective_us": (getattr(getattr(tr, "peer", None), "timing_us", None))},
+                   "exchange_vs_collective_us": (getattr(getattr(tr, "peer", None), "timing_us", None)),
+                   # (in-reduction exchange, reduce -> exchange + Adam): device us per step, MAX over
+                   # ranks, measured on the first data-parallel step; the faster form is used
+                   "fused_vs_two_launch_us": getattr(tr, "fused_vs_two_launch_us", None)},
         "mean_loss": round(loss, 5),
         "deterministic_ms_per_step": round(det_ms, 4) if det_ms is not None else None,
     }
@@ -801,6 +868,11 @@ def run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, 
     held.clear()
     gc.collect()
     torch.cuda.empty_cache()
+    if world == 1 and not args.no_train_entry:  # training.train() itself, on the headline config
+        result["train_entry"] = train_entry_leg(dev, args.config)
+        result["train_entry_pairs_per_s"] = result["train_entry"]["train_entry_pairs_per_s"]
+        gc.collect()
+        torch.cuda.empty_cache()
     if not args.no_contrastive:
         result["contrastive"] = contrastive_leg(dev, pg, world, rank,
                                                 cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))

@@ -39,7 +39,8 @@ EXPORTED = ("tt_abi_version", "tt_struct_size", "tt_stream_copy", "tt_param_coun
             "tt_adam_apply", "tt_cosine_forward", "tt_cosine_mse_fwd_bwd",
             "tt_nce_workspace_bytes", "tt_nce_norms", "tt_nce_forward", "tt_nce_loss", "tt_nce_backward",
             "tt_rank_workspace_bytes", "tt_retrieval_ranks", "tt_step_plan",
-            "tt_nce_maxes", "tt_nce_forward_lse", "tt_nce_loss_lse", "tt_nce_backward_lse")
+            "tt_nce_maxes", "tt_nce_forward_lse", "tt_nce_loss_lse", "tt_nce_backward_lse",
+            "tt_range_push", "tt_range_pop", "tt_randperm")
 
 
 class NativeLibraryError(RuntimeError):
@@ -99,6 +100,9 @@ def lib() -> ctypes.CDLL:
     H = ctypes.POINTER(TTAdamHP)
     sig = {
         "tt_abi_version": (I32, []),
+        "tt_range_push": (None, [ctypes.c_char_p]),
+        "tt_range_pop": (None, []),
+        "tt_randperm": (I32, [I64, U64, P]),
         "tt_struct_size": (I64, [I32]),
         "tt_stream_copy": (I32, [P, P, I64, P]),
         "tt_param_count": (I64, [D]),
@@ -277,3 +281,32 @@ def adam_hp(lr: float, betas=(0.9, 0.999), eps: float = 1e-8) -> TTAdamHP:
     h = TTAdamHP()
     h.lr, h.beta1, h.beta2, h.eps = float(lr), float(betas[0]), float(betas[1]), float(eps)
     return h
+
+
+class trace_range:
+    """``with trace_range("name"):`` -- a roctx range (tt_range_push / pop)
+    around host code, e.g. bench.py's timed region and graph replays."""
+
+    def __init__(self, name: str):
+        self.name = name.encode()
+
+    def __enter__(self):
+        lib().tt_range_push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        lib().tt_range_pop()
+        return False
+
+
+def randperm(n: int, seed: int, pin: bool = False):
+    """torch.randperm(n, generator=torch.Generator().manual_seed(seed)) on the
+    host, bit for bit (tt_randperm: the same mt19937 Fisher-Yates with the
+    swap targets prefetched).  None when the library does not cover n."""
+    import torch
+    out = torch.empty(n, dtype=torch.int64, pin_memory=pin)
+    rc = lib().tt_randperm(int(n), int(seed) & ((1 << 64) - 1), out.data_ptr() if n else None)
+    if rc == TT_ERR_UNSUPPORTED:
+        return None
+    check(rc, "tt_randperm")
+    return out

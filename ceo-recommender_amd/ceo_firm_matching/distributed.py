@@ -47,9 +47,8 @@ def rank_epoch_order(n: int, epoch: int, rank: int, world: int, shuffle: bool = 
         per = -(-n // world)
     total = per * world
     if shuffle:
-        g = torch.Generator()
-        g.manual_seed(seed + epoch)
-        idx = torch.randperm(n, generator=g)
+        from .training import host_randperm
+        idx = host_randperm(n, seed + epoch)  # torch.randperm(n, generator seeded seed + epoch), bit for bit
     else:
         idx = torch.arange(n, dtype=torch.int64)
     if total > n:
@@ -76,6 +75,25 @@ def average_gradients_(flat_grad: torch.Tensor, group=None) -> torch.Tensor:
     if w > 1:
         flat_grad.mul_(1.0 / w)
     return flat_grad
+
+
+def agree_exchange_form(ok: bool, t_fused_us: float, t_two_us: float, group=None, device=None,
+                        prefer_fused: bool = False):
+    """One choice of the data-parallel exchange form for every rank
+    (engine.FusedTrainer._validate_fused_exchange): the exchange inside the
+    step's reduction is kept only if EVERY rank's bitwise check passed and the
+    slowest rank's fused step (MAX over ranks) is not slower than the slowest
+    rank's reduce -> exchange + Adam step.  Returns (use_fused, (fused_us,
+    two_launch_us)) with the MAX-over-ranks times (inf where not measured).
+    ``prefer_fused`` (CEO_TT_FUSED_EX=1, tests): the bitwise check alone decides."""
+    bad = 0.0 if ok else 1.0
+    if group is not None and dist.is_available() and dist.is_initialized():
+        dev = device if dist.get_backend(group) == "nccl" else "cpu"
+        v = torch.tensor([bad, float(t_fused_us), float(t_two_us)], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+        bad, t_fused_us, t_two_us = (float(x) for x in v.cpu())
+    use = bad == 0.0 and (prefer_fused or t_fused_us <= t_two_us)
+    return use, (round(t_fused_us, 2), round(t_two_us, 2))
 
 
 def broadcast_state_(params: torch.Tensor, buffers: Optional[torch.Tensor] = None, group=None, src: int = 0):

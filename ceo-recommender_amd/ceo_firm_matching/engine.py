@@ -17,12 +17,13 @@ flat fp32 gradient is all-reduced (AVG, one call per step), and
 """
 from __future__ import annotations
 
+import weakref
 from typing import Dict, Optional
 
 import torch
 
 from . import _native as N
-from .distributed import PeerExchange, average_gradients_, broadcast_state_, world_of
+from .distributed import PeerExchange, agree_exchange_form, average_gradients_, broadcast_state_, world_of
 from .model import CEOFirmMatcher, check_category_codes
 
 DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")
@@ -67,11 +68,15 @@ class FusedTrainer:
         # GPU: a rank spinning in its reduction holds LDS and wave slots that a
         # co-located rank's forward kernels need, so ranks sharing a device
         # (rehearsals) keep the two-launch form unless CEO_TT_FUSED_EX=1
-        # (tests with small kernels); CEO_TT_FUSED_EX=0 turns it off
+        # (tests with small kernels: the bitwise check alone then decides,
+        # not the timing); CEO_TT_FUSED_EX=0 turns it off
         import os
         fx = os.environ.get("CEO_TT_FUSED_EX")
         self.fused_exchange = None if self.peer is not None and fx != "0" and (
             self.peer.co_ranks == 1 or fx == "1") else False
+        # (fused, two-launch) device us per step, MAX over ranks, measured by
+        # _validate_fused_exchange on the first data-parallel step
+        self.fused_vs_two_launch_us = None
         # TT_FLAG_DEFER_LATE: each single-GPU step leaves the late half of its
         # reduction (W4, BN1 affine, W8, logit_scale, the loss) to the next
         # step's first kernel; flush() finishes it (run automatically before
@@ -90,6 +95,9 @@ class FusedTrainer:
     def ensure_batch(self, max_batch: int):
         if max_batch <= self.max_batch:
             return
+        # a pending late half lives in the workspace (slabs, replicas, the
+        # deferral record): finish it before the workspace is replaced
+        self.flush()
         self.ws_bytes = N.workspace_bytes(self.desc, max_batch)
         self.ws = torch.zeros(self.ws_bytes // 4, dtype=torch.float32, device=self.device)
         self.max_batch = max_batch
@@ -157,7 +165,7 @@ class FusedTrainer:
         N.check(rc, "tt_train_step", n_rows, 64)
         if defer:
             self._late_rows, self._late_batch = n_rows, batch
-            self.model._pending_flush = self.flush
+            self.model._pending_flush = weakref.WeakMethod(self.flush)
         elif self._late_rows:  # (consumed by this step's first kernel)
             self._late_rows, self._late_batch = 0, None
             self.model._pending_flush = None
@@ -188,7 +196,7 @@ class FusedTrainer:
         last replayed step's late half.  The device guard makes a flush of
         nothing a no-op, never a second late half."""
         self._late_rows, self._late_batch = state
-        self.model._pending_flush = self.flush if state[0] else None
+        self.model._pending_flush = weakref.WeakMethod(self.flush) if state[0] else None
 
     def _launch_dp(self, batch, n_rows):
         """The data-parallel step: the exchange inside the step's reduction
@@ -241,6 +249,7 @@ class FusedTrainer:
         prev_det = self.deterministic
         self.deterministic = True
         N.set_deterministic(self.desc, True)
+        t_fused = t_two = float("inf")
         try:
             rc = self.peer.train_step(self, batch)
             ok = rc == N.TT_OK
@@ -252,15 +261,51 @@ class FusedTrainer:
             two = result()
             ok = ok and not self.peer.failed() and torch.equal(fused, two)
             restore()
+            # then by speed, in the mode the steps will run in: k steps of
+            # each form from the saved state (state restored after each)
+            self.deterministic = prev_det
+            N.set_deterministic(self.desc, self.is_deterministic())
+            if ok:
+                t_fused = self._time_steps(lambda: self.peer.train_step(self, batch))
+                ok = not self.peer.failed()
+                restore()
+
+                def two_launch():
+                    self._launch(batch, n_rows, False)
+                    self.allreduce_and_adam()
+                t_two = self._time_steps(two_launch)
+                ok = ok and not self.peer.failed()
+                restore()
         finally:
             self.deterministic = prev_det
             N.set_deterministic(self.desc, self.is_deterministic())
+        import os
+        use, times = agree_exchange_form(ok, t_fused, t_two, self.pg, self.device,
+                                         prefer_fused=os.environ.get("CEO_TT_FUSED_EX") == "1")
+        self.fused_vs_two_launch_us = times
+        return use
+
+    def _time_steps(self, fn, k: int = 8) -> float:
+        """Device time per step (us) of k back-to-back calls of ``fn``: the
+        launches queue behind a short GPU spin so the events bracket the
+        kernels, not the host's enqueue rate."""
+        import torch.distributed as dist
+        torch.cuda.synchronize(self.device)
         if self.pg is not None:
-            dev = self.device if dist.get_backend(self.pg) == "nccl" else "cpu"
-            flag = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.pg)
-            ok = bool(flag.item())
-        return ok
+            dist.barrier(group=self.pg)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        try:
+            torch.cuda._sleep(2_000_000)  # ~1 ms: the host enqueues the k steps meanwhile
+        except Exception:  # noqa: BLE001 -- timing then includes the host's enqueue rate
+            pass
+        e0.record()
+        for _ in range(k):
+            rc = fn()
+            if rc is not None and rc != N.TT_OK:
+                N.check(rc, "exchange timing step")
+        e1.record()
+        torch.cuda.synchronize(self.device)
+        return 1e3 * e0.elapsed_time(e1) / k
 
     def step(self, rows: Optional[torch.Tensor], row0: int, n_rows: int):
         """One optimizer step on dataset rows rows[row0:row0+n_rows]."""

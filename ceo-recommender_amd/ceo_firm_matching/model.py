@@ -76,9 +76,27 @@ class CEOFirmMatcher(nn.Module):
         self._pending_flush = None
 
     def sync_trainer(self):
-        """Finish a deferred optimizer step of the training engine, if any."""
-        if self._pending_flush is not None:
-            self._pending_flush()
+        """Finish a deferred optimizer step of the training engine, if any.
+        The trainer is held through a weak reference (engine.FusedTrainer
+        registers ``weakref.WeakMethod(trainer.flush)``): the model does not
+        keep a trainer and its workspace alive."""
+        ref = self._pending_flush
+        if ref is not None:
+            fn = ref()
+            if fn is not None:
+                fn()
+            self._pending_flush = None
+
+    def __getstate__(self):
+        """copy.deepcopy / pickle / torch.save of the module: finish a pending
+        deferred step first, and leave out the engine's handles (the weak
+        trainer reference, the ctypes arena descriptor) -- the copy binds its
+        own arena on first use on a HIP device."""
+        self.sync_trainer()
+        state = self.__dict__.copy()
+        state["_pending_flush"] = None
+        state["_arena"] = None
+        return state
 
     def state_dict(self, *args, **kwargs):
         self.sync_trainer()

@@ -4,8 +4,10 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <random>
 
 #include <hip/hip_ext.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "tt_common.h"
 #include "tt_tower.hip"
@@ -27,6 +29,17 @@ extern "C" int32_t tt_debug_set_stamps(uint64_t* buf) {
 namespace tt {
 
 constexpr size_t LDS_MAX = 160 * 1024;
+
+// roctx range around one host entry (the step and the exchange
+// attributed per rank in a rocprofv3 --marker-trace; without a profiler the
+// calls return at once).  Host code only: enqueue-side ranges, the kernels'
+// own times come from the kernel trace.
+struct Range {
+  explicit Range(const char* m) { roctxRangePushA(m); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
+};
 
 // ---------------------------------------------------------------------------
 // layouts
@@ -165,6 +178,9 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
   W.tgw = take(rows * 2);
   // slab / deterministic-slot rows: one per 64-row tile, or per 32-row
   // k_top_pair tile of a batch below TT_PAIR32_MAX_B (twice as many)
+  static_assert(TT_FWD32_MAX_B <= TT_PAIR32_MAX_B && TT_BWD32_MAX_B <= TT_PAIR32_MAX_B,
+                "the 32-row tile counts of k_l0_fwd / k_l4_fwd / k_bwd_mid / k_bwd_first index the slab and "
+                "det-slot rows sized from TT_PAIR32_MAX_B");
   const int64_t srows = std::max<int64_t>(W.n_tiles, std::min<int64_t>(2 * W.n_tiles, 2 * (TT_PAIR32_MAX_B / ROWS) + 2));
   for (int t = 0; t < 2; ++t) W.slab[t] = take(srows * L.slab_ld);
   for (int t = 0; t < 2; ++t) W.det[t] = take(srows * DET_W);
@@ -816,6 +832,11 @@ extern "C" {
 
 int32_t tt_abi_version(void) { return TT_ABI_VERSION; }
 
+void tt_range_push(const char* message) {
+  if (message) roctxRangePushA(message);
+}
+void tt_range_pop(void) { roctxRangePop(); }
+
 int64_t tt_struct_size(int32_t which) {
   switch (which) {
     case TT_STRUCT_MODEL_DESC: return (int64_t)sizeof(tt_model_desc);
@@ -1106,6 +1127,7 @@ int32_t tt_train_flush(const tt_model_desc* d, float* params, float* buffers, in
   red_step_fields(lr, RED_LATE, c.W, w, b->n_rows, state, 1, params, exp_avg, exp_avg_sq, hp,
                   reinterpret_cast<AdamSlot*>(w + c.W.adam));
   const LateRed late = to_late(lr);
+  Range rg("tt_train_flush");
   hipLaunchKernelGGL(k_reduce_late, dim3((unsigned)(late.vn / RED_E)), dim3(RED_E * LATE_G), 0, s, late);
   hipLaunchKernelGGL(k_clear_late, dim3(1), dim3(1), 0, s, late.late_pending);
   return launch_check();
@@ -1115,6 +1137,11 @@ int32_t tt_train_steps(const tt_model_desc* d, float* params, float* buffers, in
                        const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws, int64_t ws_bytes, float* grad,
                        float* exp_avg, float* exp_avg_sq, int32_t n_steps, tt_stream_t stream) {
   if (!b || b->cycle <= 0 || n_steps < 0) return TT_ERR_ARG;  // the batch must follow the device step counter
+  // a deferred late half needs the caller's pending record between steps
+  // (TT_FLAG_LATE_PENDING on the next call, tt_train_flush at the end): with
+  // the flags passed unchanged to every step, n - 1 late halves would be lost
+  if (d && (d->flags & (TT_FLAG_DEFER_LATE | TT_FLAG_LATE_PENDING))) return TT_ERR_UNSUPPORTED;
+  Range rg("tt_train_steps");
   for (int32_t k = 0; k < n_steps; ++k) {
     const int32_t rc = train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg,
                                        exp_avg_sq, 1, stream, nullptr);
@@ -1126,6 +1153,7 @@ int32_t tt_train_steps(const tt_model_desc* d, float* params, float* buffers, in
 int32_t tt_train_step(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt, const tt_batch* b,
                       const tt_adam_hp* hp, uint64_t seed, tt_state* state, void* ws, int64_t ws_bytes, float* grad,
                       float* exp_avg, float* exp_avg_sq, int32_t apply_adam, tt_stream_t stream) {
+  Range rg("tt_train_step");
   return train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg, exp_avg_sq,
                          apply_adam, stream, nullptr);
 }
@@ -1159,6 +1187,7 @@ int32_t tt_train_step_dp(const tt_model_desc* d, float* params, float* buffers, 
   x.world = world;
   x.err = err;
   x.wait_ticks = (uint64_t)(wait_us > 0 ? wait_us : 2000000) * 100ull;  // s_memrealtime: 100 MHz
+  Range rg("tt_train_step_dp");
   return train_step_impl(d, params, buffers, nbt, b, hp, seed, state, ws, ws_bytes, grad, exp_avg, exp_avg_sq, 1,
                          stream, nullptr, &x, co_ranks);
 }
@@ -1248,6 +1277,42 @@ int32_t tt_stream_copy(const void* src, void* dst, int64_t bytes, tt_stream_t st
   return (int32_t)hipGetLastError();
 }
 
+// One epoch's sample order of DataLoader(shuffle=True): torch 2.10's CPU
+// randperm(n, generator seeded with `seed`) -- the mt19937 stream of the
+// generator (32-bit seed, 32-bit outputs) driving the Fisher-Yates swaps
+// out[i] <-> out[i + mt() % (n - i)] -- bit for bit.  torch runs the swaps one
+// dependent cache miss at a time (23 ns per pair at 10M); here the swap
+// targets are drawn AHEAD steps early and their lines prefetched, so the loop
+// runs at the memory system's rate.  Host memory, no HIP call.
+int32_t tt_randperm(int64_t n, uint64_t seed, int64_t* out) {
+  if (n < 0 || (n > 0 && !out)) return TT_ERR_ARG;
+  // torch draws 64-bit randoms from n >= 2^32 / 20 on: not restated here
+  if (n >= (int64_t)(0xFFFFFFFFu / 20)) return TT_ERR_UNSUPPORTED;
+  for (int64_t i = 0; i < n; ++i) out[i] = i;
+  if (n < 2) return TT_OK;
+  std::mt19937 mt((uint32_t)seed);
+  constexpr int AHEAD = 64;  // power of two
+  uint32_t zq[AHEAD];
+  const int64_t last = n - 1;  // swaps i = 0 .. n - 2
+  int64_t drawn = 0;
+  for (; drawn < std::min<int64_t>(AHEAD, last); ++drawn) {
+    zq[drawn] = (uint32_t)(drawn + (uint32_t)mt() % (uint32_t)(n - drawn));
+    __builtin_prefetch(out + zq[drawn], 1, 0);
+  }
+  for (int64_t i = 0; i < last; ++i) {
+    const int64_t z = zq[i & (AHEAD - 1)];
+    if (drawn < last) {
+      const uint32_t zn = (uint32_t)(drawn + (uint32_t)mt() % (uint32_t)(n - drawn));
+      zq[drawn & (AHEAD - 1)] = zn;
+      __builtin_prefetch(out + zn, 1, 0);
+      ++drawn;
+    }
+    const int64_t v = out[i];
+    out[i] = out[z];
+    out[z] = v;
+  }
+  return TT_OK;
+}
 
 // ---------------------------------------------------------------------------
 // Contrastive (InfoNCE / retrieval): tt_nce_*, tt_retrieval_ranks
@@ -1730,6 +1795,7 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
   a.err = err;
   // s_memrealtime runs at 100 MHz; default bound 2 s of polling, then give up (err)
   a.wait_ticks = (uint64_t)(wait_us > 0 ? wait_us : 2000000) * 100ull;
+  Range rg("tt_ar_exchange");
   hipLaunchKernelGGL(k_ar_adam, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
   return launch_check();
 }

@@ -53,6 +53,49 @@ __device__ __forceinline__ uint64_t ld_flag(const uint64_t* f) {
   return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Step 4 for slice [lo, hi): per lane AR_EPT elements at a time, the W peer
+// slot loads of all of them (and their Adam state) issued before the first
+// wait; the own term comes from this rank's gradient (the bits its slot holds),
+// the adds run in rank order (rank_order_sums).  W >= world.
+constexpr int AR_EPT = 4;  // cfg 3: 21,313 floats / 32 blocks / 256 lanes = 2.6 per lane: one round
+template <int W>
+__device__ __forceinline__ void ar_mean_adam(const ArArgs& a, int64_t lo, int64_t hi, int64_t par,
+                                             const AdamCoef& c) {
+  const float inv_w = 1.0f / (float)a.world;
+  for (int64_t e0 = lo + threadIdx.x; e0 < hi; e0 += AR_EPT * AR_THREADS) {
+    int64_t off[AR_EPT], ec[AR_EPT];
+    float own[AR_EPT], s[AR_EPT], p[AR_EPT], m[AR_EPT], v[AR_EPT];
+#pragma unroll
+    for (int j = 0; j < AR_EPT; ++j) {  // clamped: no branch around a load
+      ec[j] = min(e0 + (int64_t)j * AR_THREADS, hi - 1);
+      off[j] = par + ec[j];
+      own[j] = a.grad[ec[j]];
+    }
+    if (a.p) {
+#pragma unroll
+      for (int j = 0; j < AR_EPT; ++j) {
+        p[j] = a.p[ec[j]];
+        m[j] = a.m[ec[j]];
+        v[j] = a.v[ec[j]];
+      }
+    }
+    rank_order_sums<W, AR_EPT>(a.slot, a.world, a.rank, off, own, s);
+#pragma unroll
+    for (int j = 0; j < AR_EPT; ++j) {
+      const int64_t e = e0 + (int64_t)j * AR_THREADS;
+      if (e >= hi) break;
+      const float g = s[j] * inv_w;
+      if (a.grad_out) a.grad_out[e] = g;
+      if (a.p) {
+        adam_elem(p[j], m[j], v[j], g, c);
+        a.p[e] = p[j];
+        a.m[e] = m[j];
+        a.v[e] = v[j];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
   // sticky failure: an earlier exchange on this rank timed out (one read per
   // block, so the whole block takes the same branch)
@@ -104,21 +147,14 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
   __syncthreads();
   if (ok_s == 0) return;  // this slice keeps its parameters (err reports it)
   // 4. mean over ranks in rank order + Adam
-  const float inv_w = 1.0f / (float)a.world;
-  for (int64_t e = lo + threadIdx.x; e < hi; e += AR_THREADS) {
-    float s = 0.f;
-    for (int q = 0; q < a.world; ++q)
-      s += __hip_atomic_load(a.slot[q] + par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const float g = s * inv_w;
-    if (a.grad_out) a.grad_out[e] = g;
-    if (a.p) {
-      float p = a.p[e], m = a.m[e], v = a.v[e];
-      adam_elem(p, m, v, g, c);
-      a.p[e] = p;
-      a.m[e] = m;
-      a.v[e] = v;
-    }
-  }
+  if (a.world <= 2)
+    ar_mean_adam<2>(a, lo, hi, par, c);
+  else if (a.world <= 4)
+    ar_mean_adam<4>(a, lo, hi, par, c);
+  else if (a.world <= 8)
+    ar_mean_adam<8>(a, lo, hi, par, c);
+  else
+    ar_mean_adam<TT_AR_MAX_RANKS>(a, lo, hi, par, c);
   if (a.p && a.state && b == 0 && threadIdx.x == 0) a.state->step_done = t;
 }
 

@@ -772,6 +772,50 @@ struct RedExchange {
   uint64_t wait_ticks;               // wait bound in s_memrealtime ticks (100 MHz)
 };
 
+// Rank-order sum of one exchanged element: the peers' slot values, this
+// rank's own term from the register (the bits its slot holds).  All W loads
+// are issued before the first add -- one s_waitcnt covers every peer's
+// system-scope read, instead of one round trip per rank over xGMI -- and the
+// adds run in rank order, so every rank computes bitwise the same sum.  W is
+// a compile-time bound >= world; lanes r >= world (and r == rank) load this
+// rank's own slot (a valid address, no branch around the load) and are
+// skipped by the uniform select.
+template <int W>
+__device__ __forceinline__ float rank_order_sum(float* const* slot, int world, int rank, int64_t off, float own) {
+  float x[W];
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    const int q = (r < world && r != rank) ? r : rank;
+    x[r] = __hip_atomic_load(slot[q] + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < W; ++r)
+    if (r < world) s += r == rank ? own : x[r];
+  return s;
+}
+// the same for EPT elements per lane (k_ar_adam): EPT x W loads in flight
+template <int W, int EPT>
+__device__ __forceinline__ void rank_order_sums(float* const* slot, int world, int rank, const int64_t* off,
+                                                const float* own, float* out) {
+  float x[EPT][W];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j)
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      const int q = (r < world && r != rank) ? r : rank;
+      x[j][r] = __hip_atomic_load(slot[q] + off[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < W; ++r)
+      if (r < world) s += r == rank ? own[j] : x[j][r];
+    out[j] = s;
+  }
+}
+
 // NS: segment capacity (the whole arena: MAX_SEG; a deferred late half,
 // LateRed below: MAX_LATE_SEG -- it rides in k_l0_fwd's kernel arguments)
 template <int NS>

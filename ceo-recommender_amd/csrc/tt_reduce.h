@@ -46,10 +46,17 @@ __device__ __forceinline__ bool reduce_exchange(const RedExchange& X, int64_t t,
   }
   __syncthreads();
   if (*ok_s == 0) return false;
-  if (owner) {
-    float s = 0.f;
-    for (int r = 0; r < X.world; ++r)
-      s += r == X.rank ? g : __hip_atomic_load(X.slot[r] + par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (owner) {  // every peer's load in flight at once (rank_order_sum), same adds as a rank loop
+    const int64_t off = par + e;
+    float s;
+    if (X.world <= 2)
+      s = rank_order_sum<2>(X.slot, X.world, X.rank, off, g);
+    else if (X.world <= 4)
+      s = rank_order_sum<4>(X.slot, X.world, X.rank, off, g);
+    else if (X.world <= 8)
+      s = rank_order_sum<8>(X.slot, X.world, X.rank, off, g);
+    else
+      s = rank_order_sum<TT_AR_MAX_RANKS>(X.slot, X.world, X.rank, off, g);
     g = s * (1.0f / (float)X.world);
   }
   return true;

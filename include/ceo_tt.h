@@ -131,6 +131,15 @@ enum {
 
 int32_t tt_abi_version(void);
 
+/* roctx ranges (rocprofiler-sdk-roctx) for callers that want their own host
+ * regions in a rocprofv3 --marker-trace beside the library's: every
+ * tt_train_step / tt_train_steps / tt_train_step_dp / tt_train_flush /
+ * tt_ar_allreduce_adam call already opens one named after the entry point.
+ * No-ops without a profiler.  (step and exchange attributed per
+ * rank; the reference has no tracing of its own.)                          */
+void tt_range_push(const char* message);
+void tt_range_pop(void);
+
 /* sizeof of the host descriptors as this library was compiled (ABI v4): a
  * binding checks its own struct definitions against them before the first
  * call (a struct a field short makes the library read past the caller's
@@ -243,7 +252,10 @@ int32_t tt_train_flush(const tt_model_desc* d, float* params, float* buffers, in
  * batches: b->cycle > 0, each step's batch taken from the device step
  * counter, so the arguments do not change between steps): the epoch loop of
  * training.py:36-57 without a host round trip per step.  Same semantics as
- * n_steps calls of tt_train_step; returns the first error.                  */
+ * n_steps calls of tt_train_step; returns the first error.  Not with
+ * TT_FLAG_DEFER_LATE / TT_FLAG_LATE_PENDING in d->flags (TT_ERR_UNSUPPORTED,
+ * nothing launched): a deferred chain needs the caller's pending record
+ * between steps -- call tt_train_step per step, then tt_train_flush.       */
 int32_t tt_train_steps(const tt_model_desc* d, float* params, float* buffers, int64_t* nbt,
                        const tt_batch* b, const tt_adam_hp* hp, uint64_t seed, tt_state* state,
                        void* ws, int64_t ws_bytes, float* grad, float* exp_avg, float* exp_avg_sq,
@@ -287,6 +299,15 @@ int32_t tt_cosine_mse_fwd_bwd(const float* u, const float* v, const float* targe
  * (bench.py's cosine roofline quotes it beside the 8 TB/s spec).  Replaces
  * nothing in the reference (a measurement probe).                           */
 int32_t tt_stream_copy(const void* src, void* dst, int64_t bytes, tt_stream_t stream);
+
+/* One epoch's batch order of DataLoader(dataset of n, shuffle=True): out[n]
+ * (host memory) = torch 2.10 CPU torch.randperm(n, generator) for a
+ * generator after manual_seed(seed) -- what RandomSampler.__iter__ draws
+ * (reference training.py:36-44 via data.py's DataLoader), bit for bit, with
+ * the Fisher-Yates swap targets prefetched ahead (no HIP call).
+ * TT_ERR_UNSUPPORTED for n >= 2^32 / 20 (torch's 64-bit draw path): the
+ * caller then uses torch.randperm.                                          */
+int32_t tt_randperm(int64_t n, uint64_t seed, int64_t* out);
 
 /* ---------------------------------------------------------------------------
  * Contrastive scoring (BASELINE cfg 5).

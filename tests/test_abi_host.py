@@ -183,6 +183,16 @@ def test_host_argument_errors():
     # cosine kernels: null pointers
     assert L.tt_cosine_forward(None, p, 8, 16, p, p, None) == N.TT_ERR_ARG
     assert L.tt_adam_apply(p, p, p, p, 10, ctypes.byref(hp), None, 0, None) == N.TT_ERR_ARG
+    # tt_train_steps cannot carry a deferred chain (the host's pending record
+    # is needed between steps): refused before anything is enqueued
+    cyc, keep3 = _batch(desc, 64)
+    cyc.cycle = 4
+    for fl in (N.TT_FLAG_DEFER_LATE, N.TT_FLAG_LATE_PENDING):
+        desc.flags |= fl
+        rc = L.tt_train_steps(ctypes.byref(desc), p, p, p, ctypes.byref(cyc), ctypes.byref(hp), 0, p, p, ws_ok,
+                              p, p, p, 3, None)
+        desc.flags &= ~fl
+        assert rc == N.TT_ERR_UNSUPPORTED, fl
 
 
 def test_product_path_refuses_without_extension(monkeypatch):

@@ -225,6 +225,70 @@ def test_info_nce_sharded_two_ranks():
         assert isinstance(err, float) and err < TOL, (rank, err)
 
 
+def _sharded_cfg5_rank(rank, world, port, q, N, D):
+    """BASELINE cfg 5 sharded across processes: rank r owns firm / CEO rows
+    [r*m, (r+1)*m) and runs info_nce_loss_sharded forward + backward -- the
+    all-gather of C (N x D fp32), the MAX all-reduce of the norms, the column
+    sum and loss all-reduces, and the dC reduction (gloo: all-reduce + slice)
+    at the production shape."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching.contrastive import info_nce_loss_sharded
+        dev = torch.device("cuda:0")
+        gen = torch.Generator().manual_seed(11)
+        f = torch.nn.functional.normalize(torch.randn(N, D, generator=gen), dim=1)
+        c = torch.nn.functional.normalize(torch.randn(N, D, generator=gen), dim=1)
+        m = N // world
+        fl = f[rank * m:(rank + 1) * m].to(dev).requires_grad_(True)
+        cl = c[rank * m:(rank + 1) * m].to(dev).requires_grad_(True)
+        del f, c
+        loss = info_nce_loss_sharded(fl, cl, 0.07)
+        loss.backward()
+        torch.cuda.synchronize()
+        q.put((rank, float(loss.detach()), fl.grad.cpu().numpy(), cl.grad.cpu().numpy()))
+    except Exception as ex:
+        q.put((rank, repr(ex), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_info_nce_sharded_eight_processes_cfg5():
+    """cfg 5 at its production shape across 8 processes (sharing the test
+    box's GPU, gloo collectives): N = 100k firms x 100k CEOs, D = 256, every
+    rank's loss, dF shard and dC shard vs the fp64 chunked reference of the
+    whole matrix at 1e-5 (contrastive.py:102-138)."""
+    dev = _dev()
+    world, N, D = 8, 100_000, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sharded_cfg5_rank, args=(r, world, port, q, N, D)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=900) for _ in ps), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=120)
+    for rank, loss, _, _ in res:
+        assert isinstance(loss, float), (rank, loss)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    gen = torch.Generator().manual_seed(11)
+    f = torch.nn.functional.normalize(torch.randn(N, D, generator=gen), dim=1).to(dev)
+    c = torch.nn.functional.normalize(torch.randn(N, D, generator=gen), dim=1).to(dev)
+    rl, rdf, rdc = _info_nce_fp64_chunked(f, c, 0.07)
+    m = N // world
+    df = torch.from_numpy(np.concatenate([r[2] for r in res])).to(dev)
+    dc = torch.from_numpy(np.concatenate([r[3] for r in res])).to(dev)
+    for rank, loss, _, _ in res:  # every rank holds the global loss
+        assert abs(loss - rl) <= TOL * abs(rl), (rank, loss, rl)
+    for got, ref in ((df, rdf), (dc, rdc)):
+        assert got.shape == ref.shape == (world * m, D)
+        err = float((got.double() - ref).abs().max() / ref.abs().max())
+        assert err < TOL, err
+
+
 # ---------------------------------------------------------------------------
 # semi_hard_negative_mining (contrastive.py:141-192) on tt_triplet_*
 # ---------------------------------------------------------------------------

@@ -50,12 +50,12 @@ def _setup(p=0.1, n_rows=8 * B, seed=5):
     }
     init = {k: torch.from_numpy(np.asarray(v)) for k, v in sub(g, "init").items()}
 
-    def make(defer, det=True):
+    def make(defer, det=True, max_batch=B):
         from ceo_firm_matching.engine import FusedTrainer
         m = CEOFirmMatcher(meta, cfg)
         m.load_state_dict(init)
         m = m.to(_dev())
-        tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=77, deterministic=det, defer_late=defer)
+        tr = FusedTrainer(m, lr=4e-4, max_batch=max_batch, seed=77, deterministic=det, defer_late=defer)
         tr.set_data({k: v.to(_dev()) for k, v in data.items()})
         return m, tr
     return g, meta, data, make
@@ -197,6 +197,31 @@ def test_batch_size_change_and_model_reads_flush():
         ok = normwise(b[k], a[k]) < 1e-5 or np.max(np.abs(b[k] - a[k])) <= 5e-2 * 4e-4 * len(sizes)
         assert ok, (k, normwise(b[k], a[k]))
     assert N.step_plan(m.tt_desc(), 12288)["folded_bn0_backward"]
+
+
+def test_workspace_growth_flushes_the_pending_late_half():
+    """A step whose batch exceeds the trainer's max_batch replaces the
+    workspace: the previous step's pending late half (its slabs, replicas and
+    deferral record live there) must run first.  Deferred steps
+    of 8192 rows on an 8192-row workspace, then 16384-row steps: the same
+    training as plain steps, loss included."""
+    _, _, data, make = _setup(p=0.0)
+    sizes = [B // 2, B // 2, B, B]
+    out = []
+    for defer in (False, True):
+        m, tr = make(defer, max_batch=B // 2)
+        off = 0
+        for bs in sizes:
+            tr.step(None, off, bs)
+            off += bs
+        assert tr.max_batch == B and tr.steps_done() == len(sizes)
+        out.append((_state(m, tr), tr.pop_loss_sum()))
+    (a, la), (b, lb) = out
+    assert abs(la - lb) <= 1e-5 * abs(la), (la, lb)
+    # parameters / moments / buffers at the optimizer-scale bound (the late
+    # half sums its slabs in another fixed order); a lost late half moves W4 /
+    # W8 / logit_scale by a whole Adam step (lr) and its loss out of the sum
+    assert np.max(np.abs(a - b)) <= 5e-2 * 4e-4 * len(sizes), np.max(np.abs(a - b))
 
 
 def test_deferred_six_kernel_path_cfg2():

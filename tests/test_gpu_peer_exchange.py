@@ -291,7 +291,7 @@ def _fused_vs_two_launch_rank(rank, world, port, q, steps):
         g = load_golden("ddp")
         shard = {k: torch.from_numpy(v) for k, v in sub(g, f"G2/shard{rank % 2}").items()}
         B = shard["target"].shape[0]
-        outs = []
+        outs, times = [], None
         for fused in (True, False):
             m = _cfg2_model(dev, g)
             tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=5, process_group=dist.group.WORLD, deterministic=True)
@@ -303,14 +303,16 @@ def _fused_vs_two_launch_rank(rank, world, port, q, steps):
                 tr.step(None, 0, B)
             tr.pop_loss_sum()
             assert tr.fused_exchange is fused, (fused, tr.fused_exchange)
+            if fused:  # validation timed both forms (device us per step, MAX over ranks)
+                times = tr.fused_vs_two_launch_us
             outs.append(np.concatenate([tr.arena.params.cpu().numpy(), tr.exp_avg.cpu().numpy(),
                                         tr.exp_avg_sq.cpu().numpy(), tr.arena.buffers.cpu().numpy()]))
             tr.peer.close()
         allo = [None] * world  # parameters and Adam moments (BN buffers are per rank: local statistics)
         dist.all_gather_object(allo, outs[0][:3 * tr.arena.params.numel()].tobytes())
-        q.put((rank, bool(np.array_equal(outs[0], outs[1])), all(a == allo[0] for a in allo)))
+        q.put((rank, bool(np.array_equal(outs[0], outs[1])), all(a == allo[0] for a in allo), times))
     except Exception as e:
-        q.put((rank, repr(e), None))
+        q.put((rank, repr(e), None, None))
         raise
     finally:
         dist.destroy_process_group()
@@ -324,9 +326,13 @@ def test_exchange_inside_reduction_matches_two_launch_form(world):
     same parameters."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    for rank, same, ranks_equal in _spawn(_fused_vs_two_launch_rank, world, 3):
+    res = _spawn(_fused_vs_two_launch_rank, world, 3)
+    for rank, same, ranks_equal, times in res:
         assert same is True, (rank, same)
         assert ranks_equal is True, rank
+        assert times is not None and all(0 < t < 1e5 for t in times), (rank, times)
+    assert len({r[3] for r in res}) == 1  # one agreed pair of timings
+    print(f"world {world}: fused vs two-launch step us {res[0][3]}")
 
 
 def test_exchange_inside_reduction_timeout_leaves_parameters():

@@ -210,3 +210,19 @@ def test_epoch_order_matches_the_dataloader(shuffle, drop_last, gen, n, bs):
     lc = make()
     it = [[int(x) for x in b[0]] for b in lc]
     assert it == [list(b) for b in ref[0]]
+
+
+@pytest.mark.parametrize("n,seed", [(0, 1), (1, 3), (2, 9), (17, 5), (4096, 2 ** 40 + 7), (1_000_003, 77),
+                                    (10_000_000, 2 ** 62 + 99)])
+def test_native_randperm_is_torch_randperm(n, seed):
+    """tt_randperm (the DataLoader order's permutation on the host, swap
+    targets prefetched) is torch 2.10's CPU randperm under manual_seed(seed),
+    bit for bit -- the 10M case is cfg 3's epoch."""
+    from ceo_firm_matching import _native as N
+    from ceo_firm_matching.training import host_randperm
+    g = torch.Generator()
+    g.manual_seed(seed)
+    ref = torch.randperm(n, generator=g)
+    got = N.randperm(n, seed)
+    assert got is not None and got.dtype == torch.int64 and torch.equal(got, ref)
+    assert torch.equal(host_randperm(n, seed), ref)

@@ -215,13 +215,20 @@ def test_workspace_growth_flushes_the_pending_late_half():
             tr.step(None, off, bs)
             off += bs
         assert tr.max_batch == B and tr.steps_done() == len(sizes)
-        out.append((_state(m, tr), tr.pop_loss_sum()))
+        loss = tr.pop_loss_sum()
+        sd = m.state_dict()
+        out.append(({k: v.detach().cpu().double().numpy().copy() for k, v in sd.items()}, loss))
     (a, la), (b, lb) = out
     assert abs(la - lb) <= 1e-5 * abs(la), (la, lb)
-    # parameters / moments / buffers at the optimizer-scale bound (the late
-    # half sums its slabs in another fixed order); a lost late half moves W4 /
-    # W8 / logit_scale by a whole Adam step (lr) and its loss out of the sum
-    assert np.max(np.abs(a - b)) <= 5e-2 * 4e-4 * len(sizes), np.max(np.abs(a - b))
+    # parameters at the optimizer-scale bound (the late half sums its slabs in
+    # another fixed order; the pre-BN biases, whose true gradient is 0, and
+    # the running means that carry them are excluded as everywhere else): a
+    # lost late half moves W4 / W8 / logit_scale by a whole Adam step (lr)
+    for k in a:
+        if excluded_param(k) or "num_batches" in k or "running_mean" in k:
+            continue
+        ok = normwise(b[k], a[k]) < 1e-5 or np.max(np.abs(b[k] - a[k])) <= 5e-2 * 4e-4 * len(sizes)
+        assert ok, (k, normwise(b[k], a[k]), np.max(np.abs(b[k] - a[k])))
 
 
 def test_deferred_six_kernel_path_cfg2():

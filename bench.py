@@ -364,15 +364,20 @@ def train_entry_leg(dev, name, timed_epochs=2):
     g = torch.Generator()
     g.manual_seed(1)
     t0 = time.perf_counter()
-    torch.randperm(n_total, generator=g)
+    ref = torch.randperm(n_total, generator=g)
     t_perm = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    mine = training.host_randperm(n_total, 1)  # what train_model's order threads run (tt_randperm)
+    t_native = time.perf_counter() - t0
+    assert torch.equal(mine, ref)
     steps = -(-n_total // B)
     return {"workload": f"{name}: train_model(DataLoader(CEOFirmDataset, batch_size={B}, shuffle=True)), "
                         f"{n_total} pairs, 1 GPU",
             "train_entry_pairs_per_s": round(n_total / per_epoch, 1), "ms_per_epoch": round(1e3 * per_epoch, 2),
             "us_per_step": round(1e6 * per_epoch / steps, 2), "steps_per_epoch": steps,
             "timed_epochs": timed_epochs, "setup_plus_first_epoch_s": round(t1, 3),
-            "host_permutation_ms_per_epoch_one_thread": round(1e3 * t_perm, 2),
+            "host_permutation_ms_per_epoch_one_thread": {"torch.randperm": round(1e3 * t_perm, 2),
+                                                         "tt_randperm": round(1e3 * t_native, 2)},
             "order_threads": training._order_ahead()}
 
 

@@ -43,6 +43,9 @@ constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 #ifndef TT_BWD32_MAX_B
 #define TT_BWD32_MAX_B 0  // (off: measured slower) unfolded batches below it run k_bwd_mid / k_bwd_first on 32-row blocks
 #endif
+#ifndef TT_L4_SHIFT_ALL
+#define TT_L4_SHIFT_ALL 0  // k_l4_fwd: every wave computes both BN1 shift tiles (no LDS hand-off / barrier)
+#endif
 #ifndef TT_FOLD_MIN_B
 #define TT_FOLD_MIN_B 8192  // smallest batch that runs the folded BN0 backward
 #endif

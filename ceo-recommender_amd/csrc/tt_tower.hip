@@ -697,7 +697,45 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
 
   // ---- Z4 = A0 W4^T (bf16x3, two K steps per 16-column tile); waves 0 and 1
   // also compute tile w of the shift row with the same MFMA sequence in every
-  // block (bitwise one shift for all blocks)
+  // block (bitwise one shift for all blocks).  TT_L4_SHIFT_ALL: every wave
+  // computes both shift tiles itself (its lanes' columns r and 16 + r), so
+  // no LDS hand-off and no barrier
+#if TT_L4_SHIFT_ALL
+  f32x4 acc[2] = {zero4(), zero4()}, accs2[2] = {zero4(), zero4()};
+  {
+    bf16x8 sa[2][3];
+    if (a.train) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const f32x4* ap = reinterpret_cast<const f32x4*>(a0r + 32 * kk + 8 * g);
+        const f32x4 p0 = ap[0], p1 = ap[1];
+        const float xs[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
+        split8x3(xs, sa[kk]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bf16x8 wf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          wf[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * j + r) * LDK + 32 * kk + 8 * g);
+        mfma_x3(xa[kk], wf, acc[j]);
+        if (a.train) mfma_x3(sa[kk], wf, accs2[j]);
+      }
+    }
+  }
+  float shv[2] = {0.f, 0.f};
+  if (a.train) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      shv[j] = accs2[j][0] + bias[j];
+      if (blockIdx.x == 0 && w == 0 && g == 0) T.shift1[16 * j + r] = shv[j];
+    }
+  }
+  (void)shl;
+#else
   f32x4 acc[2] = {zero4(), zero4()}, accs = zero4();
   {
     bf16x8 sa[2][3];
@@ -740,13 +778,17 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     }
     __syncthreads();  // shl
   }
+#endif
   TT_STAMP(1, 3);
 
   float s1[2], s2[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int col = 16 * j + r;
-    const float sh = a.train ? shl[col] : 0.f;
+#if TT_L4_SHIFT_ALL
+    const float sh = shv[j];
+#else
+    const float sh = a.train ? shl[16 * j + r] : 0.f;
+#endif
     s1[j] = 0.f;
     s2[j] = 0.f;
 #pragma unroll

@@ -52,6 +52,11 @@ def test_stub_blocks_execute_and_match_the_library():
             assert getattr(st, fn).offset == getattr(mine, fm).offset, (name, fn)
     assert L.tt_struct_size(99) == -1
     assert callable(ns["train_step"]) and callable(ns["backward_ex"]) and callable(ns["semi_hard_loss"])
+    # the DataLoader-order stub is torch's randperm under the sampler's seed
+    for n, seed in ((0, 1), (1000, 5), (100_003, 2 ** 45 + 3)):
+        g = torch.Generator()
+        g.manual_seed(seed)
+        assert torch.equal(ns["epoch_order"](n, seed), torch.randperm(n, generator=g)), (n, seed)
 
 
 @pytest.mark.gpu

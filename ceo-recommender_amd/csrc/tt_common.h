@@ -46,6 +46,9 @@ constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 #ifndef TT_L4_SHIFT_ALL
 #define TT_L4_SHIFT_ALL 0  // k_l4_fwd: every wave computes both BN1 shift tiles (no LDS hand-off / barrier)
 #endif
+#ifndef TT_PREFETCH_NEXT
+#define TT_PREFETCH_NEXT 0  // k_reduce_adam prefetches the next step's batch rows (Infinity Cache)
+#endif
 #ifndef TT_FOLD_MIN_B
 #define TT_FOLD_MIN_B 8192  // smallest batch that runs the folded BN0 backward
 #endif
@@ -852,6 +855,17 @@ struct RedArgsN {
   // step_cur meanwhile)
   int64_t* late_pending;
   int32_t late_mark;     // early half: 1 records t + 1 (deferring), -1 records 0 (not deferring), 0 leaves it
+  // TT_PREFETCH_NEXT (k_reduce_adam of a cycle-mode step): pf_blocks extra
+  // blocks after the element blocks touch every 128-B line of the NEXT step's
+  // batch rows of both towers' numeric features, so k_l0_fwd(t + 1) gathers
+  // them from the Infinity Cache instead of HBM
+  const float* pf_num[2];
+  int64_t pf_ld[2];
+  int32_t pf_cols[2];
+  const int64_t* pf_rows;
+  int64_t pf_B, pf_cycle, pf_tbase;
+  int32_t pf_blocks;
+  float* pf_sink;        // never written for finite data (keeps the loads alive)
 };
 using RedArgs = RedArgsN<MAX_SEG>;
 constexpr int MAX_LATE_SEG = 8;

@@ -619,20 +619,18 @@ def main():
         step_fn()
     torch.cuda.synchronize()
 
-    # chunks of 16 steps for long runs (measured: 10 -> 16 takes 0.8 us off a
-    # step, 20 / 25 / 40 add 0.3-1.1 us), the remainder of K in a second,
-    # shorter graph; short runs (the driver's K = 20) in 4-step graphs
-    # replayed back to back (round 5, tools/kfix_probe.py on two boxes: the
-    # first launch of a graph costs more the bigger the graph, and switching
-    # between graph objects costs more than replaying one -- K = 20 as 5 x 4
-    # took 30.5 / 46.9 us over K times the 400-step rate, 10 + 10 43.3 / 50.3)
+    # chunks of 16 steps (measured: 10 -> 16 takes 0.8 us off a step, 20 /
+    # 25 / 40 add 0.3-1.1 us), the remainder of K in a second, shorter graph.
+    # The driver's K = 20 stays two graphs of 10: round 5, five interleaved
+    # runs of the driver's command per chunk size, 53.7-53.9 us per step
+    # against 54.7-55.0 (4-step graphs) and 54.3-54.7 (5-step graphs)
     graph, graph_rem, chunk = None, None, 1
     if use_graph:
         # K split into equal graphs of at most 16 steps (the driver's K = 20:
         # two of 10 -- four interleaved rounds: 56.0-56.4 us per step against
         # 56.5-57.1 for one graph of 20 and 57.1 for 16 + 4; graphs of 4-5
         # steps 56.8-57.5)
-        cmax = int(os.environ.get("CEO_BENCH_CHUNK_MAX", "16" if args.steps > 32 else "4"))
+        cmax = int(os.environ.get("CEO_BENCH_CHUNK_MAX", "16"))
         n_graphs = -(-args.steps // cmax)
         chunk = -(-args.steps // n_graphs)
         rem = args.steps % chunk

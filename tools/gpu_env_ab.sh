@@ -1,5 +1,6 @@
 # interleaved bench rounds under different environment settings:
 #   bash tools/gpu_env_ab.sh ROUNDS "ENV1" "ENV2" ...   (ENV "-" = unchanged)
+#   STEPS / WARMUP / BENCH_ARGS override the bench arguments
 set -o pipefail
 export TMPDIR=/tmp; mkdir -p gpurun_out/envab
 R=$1; shift
@@ -9,6 +10,11 @@ for i in $(seq 1 $R); do
     j=$((j+1))
     if [ "$E" = "-" ]; then E=""; fi
     env $E timeout -k 10 200 python bench.py ${BENCH_ARGS:---no-cpu-baseline --no-contrastive --no-side-config --no-train-entry} --steps ${STEPS:-400} --warmup ${WARMUP:-20} > gpurun_out/envab/$j.$i.json 2> gpurun_out/envab/$j.$i.err || { echo "$E failed"; tail -5 gpurun_out/envab/$j.$i.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/envab/$j.$i.json'));k=d['kernel_us'];print('[$E]', d['ms_per_step'], round(d['value']/1e6,1), {a[2:]: round(b,2) for a,b in k.items()})"
+    TAG="$E" F=gpurun_out/envab/$j.$i.json python - <<'PY'
+import json, os
+d = json.load(open(os.environ["F"]))
+k = d.get("kernel_us", {})
+print("[" + os.environ["TAG"] + "]", d["ms_per_step"], round(d["value"] / 1e6, 1), {a[2:]: round(b, 2) for a, b in k.items()})
+PY
   done
 done

@@ -675,17 +675,16 @@ def main():
     if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    # roctx range around the timed region, opened before t0 and
-    # closed after the clock stops: no host call inside the region but the
-    # replays themselves (the per-step ranges are the C-ABI's own, eager steps)
-    region = N.trace_range(f"bench timed region: {args.steps} steps, rank {rank}")
-    region.__enter__()
+    region = N.trace_range(f"bench timed region: {args.steps} steps, rank {rank}")  # roctx
     t0 = time.perf_counter()
+    region.__enter__()
     if graph is not None:  # exactly K steps: K // chunk full chunks + the remainder graph
         for _ in range(args.steps // chunk):
-            graph.replay()
+            with N.trace_range(f"step chunk x{chunk}"):
+                graph.replay()
         if graph_rem is not None:
-            graph_rem.replay()
+            with N.trace_range(f"step chunk x{args.steps % chunk}"):
+                graph_rem.replay()
     elif c_steps:  # exactly K steps launched by one tt_train_steps call
         tr.step_cycle_n(rows, B, n_batches, args.steps)
     else:

@@ -1,6 +1,7 @@
 // Host side of libceo_tt.so: argument checking, arena / workspace layout and
 // kernel launch sequences behind the C-ABI declared in include/ceo_tt.h.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -449,6 +450,7 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
                  int64_t rep_stride = 0) -> bool {
     if (len <= 0) return false;
     if ((part == RED_EARLY && late_range) || (part == RED_LATE && !late_range)) return false;
+    if (k >= MAX_SEG) std::abort();  // 1 + 2 x 6 + 1 ranges at most (static_assert MAX_SEG >= 14)
     r.seg[k].off = off;
     r.seg[k].len = len;
     r.seg[k].kind = kind;
@@ -520,6 +522,8 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   int64_t vo = 0;
   for (int j = 0; j < k; ++j) {
     const int i = order[j];
+    r.blk0[j] = (int32_t)(vo / RED_E);
+    r.blk_seg[j] = i;
     r.seg[i].voff = vo;
     const int64_t len = r.seg[i].len;
     r.seg[i].vlen = r.seg[i].kind == 3 ? 2 * len : r.seg[i].kind == 5 ? (len + 31) / 32 * 64 : len;
@@ -578,7 +582,11 @@ static void red_step_fields(A& r, int part, const WsLayout& W, float* w, int64_t
 static LateRed to_late(const RedArgs& r) {
   LateRed q;
   std::memset(&q, 0, sizeof(q));
-  for (int i = 0; i < r.n_seg; ++i) q.seg[i] = r.seg[i];
+  for (int i = 0; i < r.n_seg; ++i) {
+    q.seg[i] = r.seg[i];
+    q.blk0[i] = r.blk0[i];
+    q.blk_seg[i] = r.blk_seg[i];
+  }
 #define TT_CP(f) q.f = r.f;
   TT_CP(n_seg) TT_CP(n_slabs) TT_CP(n) TT_CP(vn) TT_CP(slab_ld) TT_CP(gacc) TT_CP(grad) TT_CP(lsr) TT_CP(loss_state)
   TT_CP(apply_adam) TT_CP(p) TT_CP(m) TT_CP(v) TT_CP(lr) TT_CP(b1) TT_CP(b2) TT_CP(eps) TT_CP(adam_slots)

@@ -736,7 +736,12 @@ __device__ __forceinline__ float tower_x(const TowerDev& T, int64_t drow, int co
 // ---------------------------------------------------------------------------
 // gradient reduction / Adam arguments (tt_optim.hip)
 // ---------------------------------------------------------------------------
-constexpr int MAX_SEG = 48;
+#ifndef TT_MAX_SEG
+#define TT_MAX_SEG 16  // was 48: 5.2 KB of kernel arguments per k_reduce_adam launch, now 1.9 KB
+#endif
+// segment capacity of a reduction (make_red adds at most 1 + 2 x 6 + 1 = 14)
+constexpr int MAX_SEG = TT_MAX_SEG;
+static_assert(MAX_SEG >= 14, "make_red's ranges: embeddings, 6 per tower, logit_scale");
 #ifndef TT_RED_MINW
 #define TT_RED_MINW 7  // waves per SIMD: <= 73 VGPRs (no spills with 16 loads in flight); 9.4 us vs 10.8 at 8
 #endif
@@ -827,6 +832,13 @@ __device__ __forceinline__ void rank_order_sums(float* const* slot, int world, i
 template <int NS>
 struct RedArgsN {
   Seg seg[NS];
+  // the segments in element-space (block) order: entry j covers blocks
+  // [blk0[j], blk0[j + 1]) and is seg[blk_seg[j]] -- a block finds its
+  // segment from these two compact arrays (one scalar-load round trip and
+  // SALU compares) instead of walking seg[] with a dependent kernel-argument
+  // load per segment (the last ranges paid ~12 of them: DESIGN 14b)
+  int32_t blk0[NS];
+  int32_t blk_seg[NS];
   int32_t n_seg;
   int32_t n_slabs;
   int64_t n;

@@ -51,11 +51,13 @@ __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedAr
   __shared__ float part[RED_G * RED_E];
   __shared__ float xpart[4 * RED_G * RED_E];  // kinds 3, 4: gg0, gbe0, sum Zh0, sum X' replicas
   __shared__ int xok_s;
+#if TT_PREFETCH_NEXT
   const int nb = (int)(a.vn / RED_E);
   if ((int)blockIdx.x >= nb) {  // (whole block: uniform)
     prefetch_next_rows(a, (int)blockIdx.x - nb);
     return;
   }
+#endif
   reduce_body<RedArgs, RED_G, PRE, EX, false>(a, (int)blockIdx.x, part, xpart, &xok_s);
 }
 

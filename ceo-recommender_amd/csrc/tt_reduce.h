@@ -89,11 +89,15 @@ __device__ __forceinline__ void reduce_body(const A& a, int bid, float* part, fl
   }
   const int el = threadIdx.x & (RED_E - 1), pg = threadIdx.x / RED_E;
   const int64_t vb = (int64_t)bid * RED_E;
+  // this block's segment: the last entry (block order) starting at or
+  // before it, from the compact blk0 / blk_seg arrays -- loaded together,
+  // compared in SALU (no dependent load per segment)
   int si = -1;
-  for (int k = 0; k < a.n_seg; ++k)
-    if (vb >= a.seg[k].voff && vb < a.seg[k].voff + a.seg[k].vlen) { si = k; break; }
+#pragma unroll
+  for (int j = 0; j < (int)(sizeof(a.blk0) / sizeof(a.blk0[0])); ++j)
+    if (j < a.n_seg && bid >= a.blk0[j]) si = a.blk_seg[j];
   si = __builtin_amdgcn_readfirstlane(si);
-  if (si < 0) return;  // padding between ranges (whole block)
+  if (si < 0 || vb >= a.seg[si].voff + a.seg[si].vlen) return;  // (whole block: past the last range)
   const Seg& S = a.seg[si];
   const int kind = S.kind;
   const int64_t dv = vb + el - S.voff;

@@ -9,8 +9,13 @@ for i in $(seq 1 $R); do
   for E in "$@"; do
     j=$((j+1))
     if [ "$E" = "-" ]; then E=""; fi
-    env $E timeout -k 10 200 python bench.py ${BENCH_ARGS:---no-cpu-baseline --no-contrastive --no-side-config --no-train-entry} --steps ${STEPS:-400} --warmup ${WARMUP:-20} > gpurun_out/envab/$j.$i.json 2> gpurun_out/envab/$j.$i.err || { echo "$E failed"; tail -5 gpurun_out/envab/$j.$i.err; exit 1; }
-    TAG="$E" F=gpurun_out/envab/$j.$i.json python - <<'PY'
+    B=bench.py; EE=""
+    for tok in $E; do
+      case "$tok" in BENCH=*) B="${tok#BENCH=}";; *) EE="$EE $tok";; esac
+    done
+    E="$EE"
+    env $E timeout -k 10 200 python $B ${BENCH_ARGS:---no-cpu-baseline --no-contrastive --no-side-config --no-train-entry} --steps ${STEPS:-400} --warmup ${WARMUP:-20} > gpurun_out/envab/$j.$i.json 2> gpurun_out/envab/$j.$i.err || { echo "$E failed"; tail -5 gpurun_out/envab/$j.$i.err; exit 1; }
+    TAG="$E $B" F=gpurun_out/envab/$j.$i.json python - <<'PY'
 import json, os
 d = json.load(open(os.environ["F"]))
 k = d.get("kernel_us", {})

@@ -11,7 +11,7 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench_k20.
 python -c "import json;d=json.load(open('$D/bench_k20.json'));print('K20', d['ms_per_step'], round(d['value']/1e6,1), d['roofline']['frac'])"
 timeout -k 10 300 python bench.py > $D/bench.json 2> $D/bench.err || { tail -20 $D/bench.err; exit 1; }
 python -c "import json;d=json.load(open('$D/bench.json'));print('K400', d['ms_per_step'], round(d['value']/1e6,1), d['kernel_us'], d['roofline']['frac'])"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-contrastive > $D/prof.log 2>&1 || { rc=$?; tail -20 $D/prof.log; exit $rc; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-contrastive --no-train-entry > $D/prof.log 2>&1 || { rc=$?; tail -20 $D/prof.log; exit $rc; }
 find $D/prof -name "*kernel_stats.csv"
 bash tools/pmc_profile.sh $T/pmc > $D/pmc.log 2>&1 || { tail -20 $D/pmc.log; exit 1; }
 python tools/pmc_traffic.py $D/pmc $D/pmc_traffic.json && echo pmc ok

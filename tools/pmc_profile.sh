@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
-BENCH="bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-graph --no-side-config --no-contrastive $@"
+BENCH="bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-graph --no-side-config --no-contrastive --no-train-entry $@"
 i=0
 for SET in \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \

@@ -49,6 +49,12 @@ constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 #ifndef TT_PREFETCH_NEXT
 #define TT_PREFETCH_NEXT 0  // k_reduce_adam prefetches the next step's batch rows (Infinity Cache)
 #endif
+#ifndef TT_FOLD_REP_FIRST
+#define TT_FOLD_REP_FIRST 0  // k_bwd_mid_fold: BN1-affine replica loads issued first (RepSum1)
+#endif
+#ifndef TT_PAIR_REP_FIRST
+#define TT_PAIR_REP_FIRST 0  // k_top_pair: BN1 moment replica loads issued first
+#endif
 #ifndef TT_FOLD_MIN_B
 #define TT_FOLD_MIN_B 8192  // smallest batch that runs the folded BN0 backward
 #endif

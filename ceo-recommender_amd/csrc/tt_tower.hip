@@ -1349,6 +1349,12 @@ __global__ __launch_bounds__(R * 8) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs 
 
   // ---- phase 0: every load -- own tower's Z4 slice, both W8 (raw), biases,
   // logit_scale, (target, weight), BN1 inputs, BN1 moment replicas
+  // (TT_PAIR_REP_FIRST: the replicas first, so their sum and the coefficient
+  // chain wait for them alone)
+#if TT_PAIR_REP_FIRST
+  RepSum2<NTH, 2 * H1> rs;
+  rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
+#endif
   float4 zs[2];
   {
     const float4* ps_ = reinterpret_cast<const float4*>(T.Z4 + row * H1 + 8 * g);
@@ -1377,8 +1383,10 @@ __global__ __launch_bounds__(R * 8) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs 
     bn_g = g1p[bc];
     bn_be = pick(bt, a.tw[0].be1, a.tw[1].be1)[bc];
   }
+#if !TT_PAIR_REP_FIRST
   RepSum2<NTH, 2 * H1> rs;
   rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
+#endif
   if (threadIdx.x < 2 * DP) smem[L::b8s + threadIdx.x] = (threadIdx.x % DP) < (unsigned)D ? b8v : 0.f;
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
@@ -1892,7 +1900,13 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
 
   // ---- phase 0: issue every load -- dY1, Z4, Z0 of this wave's rows (C
   // layout), W4, BN inputs, then (after the step load they depend on) the
-  // dataset rows of this thread's X' gather rows and of the shift row
+  // dataset rows of this thread's X' gather rows and of the shift row.
+  // TT_FOLD_REP_FIRST: the BN1-affine replicas first, so their sum and the
+  // coefficient chain wait for them alone (vmcnt retires in issue order)
+#if TT_FOLD_REP_FIRST
+  RepSum1<NTH, 2 * H1> rs1;
+  rs1.issue(T.gg1, BNG);
+#endif
   f32x4 dy1[2], zz4[2], zz0[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1926,7 +1940,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
 #pragma unroll
   for (int k = 0; k < XK; ++k) xrow[k] = data_row_nb(a, base, min(r0 + xr0 + k, a.B - 1));
   const int64_t crow = data_row_nb(a, base, 0);
+#if TT_FOLD_REP_FIRST
+  rs1.finish(smem + L::rsc, smem + L::rst);
+#else
   rep_sum<NTH, 2 * H1>(T.gg1, BNG, smem + L::rsc, smem + L::rst);  // gg1|gbe1 are adjacent in a replica
+#endif
   {
     const float* rst = smem + L::rst;
     if (threadIdx.x < H1) {

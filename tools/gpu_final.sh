@@ -15,3 +15,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-fo
 find $D/prof -name "*kernel_stats.csv"
 bash tools/pmc_profile.sh $T/pmc > $D/pmc.log 2>&1 || { tail -20 $D/pmc.log; exit 1; }
 python tools/pmc_traffic.py $D/pmc $D/pmc_traffic.json && echo pmc ok
+# roctx ranges: the step / exchange entry points and bench's timed region in a marker trace
+timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats -d $D/markers -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline > $D/markers.log 2>&1 || { rc=$?; tail -20 $D/markers.log; exit $rc; }
+find $D/markers -name "*.csv" | head

@@ -271,10 +271,11 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   // kernel reads was written earlier in the same step
   P->n_tiles = (int)(padded_rows(B) / ROWS);
   P->n_tiles_top = (int)((P->n_tiles * ROWS) / P->top_rows);
-  // folded only for batches that still give the 128-row kernel >= 64 tiles
-  // per tower: cfg 2 (B = 4096) measured 45.9 us folded vs 42.4 us not (r01);
-  // re-measured with this round's kernels: 44.1 vs 43.7 us (k_bwd_mid_fold
-  // takes 14.1 us on its 64 blocks: its per-block chain, not bandwidth)
+  // folded from B = 4096 (32 blocks of 128 rows per tower): cfg 2 measured
+  // 45.9 us folded vs 42.4 us not (r01), 44.1 vs 43.7 (r03); round 5, with
+  // the reduction's segment lookup fixed and k_top_pair on 32-row blocks
+  // below 8192 (TT_PAIR32_FOLD): 38.1-38.2 us folded vs 40.0-40.1 not
+  // (three interleaved rounds)
   P->fold = L.fold_ok && B >= TT_FOLD_MIN_B;
   P->bwd_rows = !P->fold && B < TT_BWD32_MAX_B ? 32 : ROWS;
   P->n_tiles_mid = (int)((P->n_tiles * ROWS) / (P->fold ? FOLD_ROWS : P->bwd_rows));
@@ -287,7 +288,7 @@ static int make_plan(const tt_model_desc* d, const Layout& L, int64_t B, Plan* P
   // below the folded path the 64-row k_top_pair leaves CUs idle (cfg 2: 64
   // blocks on 256 CUs): 32-row blocks there (TT_PAIR32_MAX_B = 0: never)
 #ifndef TT_PAIR32_FOLD
-#define TT_PAIR32_FOLD 0  // probe (measured slower at cfg 3): 32-row k_top_pair on the folded path too
+#define TT_PAIR32_FOLD 1  // 32-row k_top_pair on the folded path below TT_PAIR32_MAX_B too (cfg 2: 38.9 -> 38.2 us)
 #endif
   P->pair_rows = P->top_pair && (!P->fold || TT_PAIR32_FOLD) && B < TT_PAIR32_MAX_B ? 32 : 64;
   P->fwd_rows = !P->fold && B < TT_FWD32_MAX_B ? 32 : 64;

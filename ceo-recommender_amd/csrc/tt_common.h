@@ -56,7 +56,7 @@ constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 #define TT_PAIR_REP_FIRST 0  // k_top_pair: BN1 moment replica loads issued first
 #endif
 #ifndef TT_FOLD_MIN_B
-#define TT_FOLD_MIN_B 8192  // smallest batch that runs the folded BN0 backward
+#define TT_FOLD_MIN_B 4096  // smallest batch that runs the folded BN0 backward (round 5: cfg 2 40.0 -> 38.9 us)
 #endif
 constexpr int LSR = 32;               // replica stride of the (dls, loss) pair
 __device__ __forceinline__ int rep_of_block() { return (int)(blockIdx.x % NREP); }

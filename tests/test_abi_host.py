@@ -109,18 +109,23 @@ def test_workspace_bytes_grow_with_batch():
 
 
 def test_step_plan_tiles():
-    """tt_step_plan (host only): the folded five-kernel step from B = 8192,
-    k_top_pair from B = 4096 on 32-row blocks below the folded path, and the
-    other tower kernels' row tiles (32 below the folded path when the build
-    enables it: TT_FWD32_MAX_B / TT_BWD32_MAX_B)."""
+    """tt_step_plan (host only): the folded five-kernel step from B = 4096
+    (numeric-only towers), k_top_pair from B = 4096 on 32-row blocks below
+    8192, the six-kernel step below 4096 (and for towers with embeddings),
+    and the other tower kernels' row tiles (32 below the folded path when the
+    build enables it: TT_FWD32_MAX_B / TT_BWD32_MAX_B)."""
     desc = _model("cfg3").tt_desc()
     big = N.step_plan(desc, 16384)
     assert big["folded_bn0_backward"] and big["kernels"] == 5 and big["mid_rows"] == 128
     assert big["top_pair"] and big["train_top_rows"] == 64 and big["fwd_rows"] == 64
     mid = N.step_plan(desc, 6000)
-    assert not mid["folded_bn0_backward"] and mid["kernels"] == 6
+    assert mid["folded_bn0_backward"] and mid["kernels"] == 5 and mid["mid_rows"] == 128
     assert mid["top_pair"] and mid["train_top_rows"] == 32
-    assert mid["fwd_rows"] in (32, 64) and mid["mid_rows"] in (32, 64)
+    low = N.step_plan(desc, 3000)
+    assert not low["folded_bn0_backward"] and low["kernels"] == 6 and not low["top_pair"]
+    assert low["fwd_rows"] in (32, 64) and low["mid_rows"] in (32, 64)
+    emb = N.step_plan(_model("meta_test").tt_desc(), 6000)  # embeddings: never folded
+    assert not emb["folded_bn0_backward"] and emb["kernels"] == 6 and emb["train_top_rows"] == 32
     small = N.step_plan(desc, 1000)
     assert not small["top_pair"] and small["train_top_rows"] == small["top_rows"] == 64
     # the workspace covers the doubled tile count of the 32-row kernels

@@ -232,7 +232,7 @@ def test_workspace_growth_flushes_the_pending_late_half():
 
 
 def test_deferred_six_kernel_path_cfg2():
-    """The cfg-2 geometry (32 x 32 features, LATENT 64, B = 4096: the
+    """The cfg-2 geometry (32 x 32 features, LATENT 64, B = 4000: the
     six-kernel path, no folded BN0 backward) deferred vs plain: the same
     training at the optimizer-scale bound, loss at 1e-5."""
     from ceo_firm_matching import CEOFirmMatcher, Config
@@ -244,7 +244,7 @@ def test_deferred_six_kernel_path_cfg2():
     cfg.LATENT_DIM = int(g["meta/latent"])
     cfg.DROPOUT_P = 0.1
     cfg.DEVICE = _dev()
-    Bc, K = 4096, 5
+    Bc, K = 4000, 5
     rng = np.random.default_rng(12)
     data = {
         "firm_numeric": torch.from_numpy(rng.standard_normal((K * Bc, meta["n_firm_numeric"])).astype(np.float32)),

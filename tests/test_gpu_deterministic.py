@@ -75,8 +75,9 @@ def _run(case, B, K, p, seed, det=True, data_seed=99):
     return sd, tr.exp_avg.cpu().numpy(), tr.exp_avg_sq.cpu().numpy(), losses, grad0, m, tr
 
 
-@pytest.mark.parametrize("case,B,p", [("meta_test", 300, 0.1), ("cfg2", 4096, 0.1), ("cfg3", 16384, 0.1)],
-                         ids=["embeddings-6k", "pair-4096", "folded-16384"])
+@pytest.mark.parametrize("case,B,p", [("meta_test", 300, 0.1), ("cfg2", 3000, 0.1), ("cfg2", 4096, 0.1),
+                                      ("cfg3", 16384, 0.1)],
+                         ids=["embeddings-6k", "unfolded-3000", "pair32-folded-4096", "folded-16384"])
 def test_deterministic_steps_are_bitwise_repeatable(case, B, p):
     a = _run(case, B, 4, p, seed=21)
     b = _run(case, B, 4, p, seed=21)

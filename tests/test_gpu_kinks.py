@@ -7,7 +7,8 @@ autograd's backward of them), WITHOUT screening or nudging the inputs.
   y = 0 exactly -- so ReLU sits exactly on its kink for every row and
   ATen's threshold_backward gives that column zero gradient; the running
   variance decays to 0.9 * rv.  Both BN layers, both towers, the six-kernel
-  path (B = 4096) and the folded cfg-3 step (B = 16384), dropout off and on,
+  path (B = 3000), the folded step on 32-row k_top_pair blocks (B = 4096)
+  and the folded cfg-3 step (B = 16384), dropout off and on,
   atomic and deterministic reductions: the fused step's gradient arena and
   the parameters after Adam at 1e-5 of the fp64 oracle;
 * unscreened data at B = 16384 (the bench batch): elements whose pre-ReLU
@@ -95,7 +96,7 @@ def _zero_columns(P):
 
 
 @pytest.mark.parametrize("det", [False, True], ids=["atomics", "deterministic"])
-@pytest.mark.parametrize("B,p", [(4096, 0.0), (4096, 0.1), (16384, 0.0), (16384, 0.1)])
+@pytest.mark.parametrize("B,p", [(3000, 0.0), (3000, 0.1), (4096, 0.0), (4096, 0.1), (16384, 0.0), (16384, 0.1)])
 def test_exact_kink_zero_variance_columns(B, p, det):
     from ceo_firm_matching import _native as N
     from oracle import two_tower as O

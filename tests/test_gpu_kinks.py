@@ -106,7 +106,7 @@ def test_exact_kink_zero_variance_columns(B, p, det):
     data = _draw(meta, B, 300 + B)
     seed = 41
     m, tr = _fused_step(g, meta, P, data, B, p, seed, det)
-    assert N.step_plan(m.tt_desc(), B)["folded_bn0_backward"] == (B >= 8192)
+    assert N.step_plan(m.tt_desc(), B)["folded_bn0_backward"] == (B >= 4096)
     masks = None
     if p > 0:
         masks = {(t, l): torch.from_numpy(O.dropout_keep_mask(seed, 1, t, l, B, H, p)).double()

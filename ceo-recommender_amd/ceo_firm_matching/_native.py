@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 
 import torch
 
-TT_ABI_VERSION = 4
+TT_ABI_VERSION = 5
 TT_MAX_CAT = 16
 TT_SLOTS_PER_TOWER = 10
 TT_NUM_OFFSETS = 2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER + 1
@@ -65,8 +65,8 @@ class TTBatch(ctypes.Structure):
 
 
 class TTAdamHP(ctypes.Structure):
-    _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float),
-                ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
+    _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double),
+                ("beta2", ctypes.c_double), ("eps", ctypes.c_double)]
 
 
 TT_AR_MAX_RANKS = 16

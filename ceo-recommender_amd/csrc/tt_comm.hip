@@ -42,7 +42,7 @@ struct ArArgs {
   const float* grad;                     // this rank's gradient (k_reduce_adam output)
   float* grad_out;                       // mean gradient (nullable)
   float *p, *m, *v;                      // Adam (nullable p: no Adam)
-  float lr, b1, b2, eps;
+  double lr, b1, b2, eps;
   tt_state* state;
   int64_t step_host;
   int32_t* err;                          // set when a wait times out

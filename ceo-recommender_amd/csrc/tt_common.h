@@ -392,23 +392,26 @@ struct TowerDev {
 
 enum TopMode : int { TOP_FWD = 0, TOP_TRAIN = 1, TOP_BWD_GIVEN = 2, TOP_EMB_FWD = 3, TOP_EMB_BWD = 4 };
 
-// Adam arithmetic of torch 2.10 _single_tensor_adam (training.py:55): bias
-// corrections in double, element math in fp32 (k_reduce_adam, k_adam,
-// k_ar_adam and k_bwd_mid_fold's side reduction)
+// Adam arithmetic of torch 2.10 _single_tensor_adam (training.py:55) from
+// the hyperparameters as Python passes them (double): bias corrections in
+// double, each scalar cast to float where torch's kernels cast it (lerp
+// weight 1 - beta1, mul_ beta2, addcmul value 1 - beta2, addcdiv value
+// -lr / bc1, the divisor sqrt(bc2), eps), element math in fp32
+// (k_reduce_adam, k_adam, k_ar_adam and k_bwd_mid_fold's side reduction)
 struct AdamCoef {
   float w1, c2, b2, step_size, bc2s, eps;
 };
 
-__device__ __forceinline__ AdamCoef adam_coef(float lr, float b1, float b2, float eps, int64_t t) {
-  const double bc1 = 1.0 - pow((double)b1, (double)t);
-  const double bc2 = 1.0 - pow((double)b2, (double)t);
+__device__ __forceinline__ AdamCoef adam_coef(double lr, double b1, double b2, double eps, int64_t t) {
+  const double bc1 = 1.0 - pow(b1, (double)t);
+  const double bc2 = 1.0 - pow(b2, (double)t);
   AdamCoef c;
-  c.w1 = (float)(1.0 - (double)b1);
-  c.c2 = (float)(1.0 - (double)b2);
-  c.b2 = b2;
-  c.step_size = (float)((double)lr / bc1);
+  c.w1 = (float)(1.0 - b1);
+  c.c2 = (float)(1.0 - b2);
+  c.b2 = (float)b2;
+  c.step_size = (float)(lr / bc1);
   c.bc2s = (float)sqrt(bc2);
-  c.eps = eps;
+  c.eps = (float)eps;
   return c;
 }
 
@@ -429,14 +432,14 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // reads of t.
 struct AdamSlot {
   int64_t t;
-  float lr, b1, b2, eps;
+  double lr, b1, b2, eps;
   AdamCoef c;
 };
-__device__ __forceinline__ bool adam_slot_ok(const AdamSlot& s, int64_t t, float lr, float b1, float b2,
-                                             float eps) {
+__device__ __forceinline__ bool adam_slot_ok(const AdamSlot& s, int64_t t, double lr, double b1, double b2,
+                                             double eps) {
   return s.t == t && s.lr == lr && s.b1 == b1 && s.b2 == b2 && s.eps == eps;
 }
-__device__ __forceinline__ void adam_slot_fill(AdamSlot& s, int64_t t, float lr, float b1, float b2, float eps) {
+__device__ __forceinline__ void adam_slot_fill(AdamSlot& s, int64_t t, double lr, double b1, double b2, double eps) {
   s.c = adam_coef(lr, b1, b2, eps, t);
   s.lr = lr;
   s.b1 = b1;
@@ -474,7 +477,7 @@ struct StepArgs {
   float* fr_zero;        // k_l0_fwd zeroes fr_zero[0, fr_zero_len) (both towers' fold replicas)
   int fr_zero_len;
   AdamSlot* adam_slots;  // non-null: k_l0_fwd makes sure slot t & 1 holds step t's coefficients
-  float adam_lr, adam_b1, adam_b2, adam_eps;
+  double adam_lr, adam_b1, adam_b2, adam_eps;
   int det;               // deterministic reductions (TT_FLAG_DETERMINISTIC): slots + k_det_fold
   float* dslot_lsr;      // det: per-block (dls, loss) partials [blocks][2]
   int xcd_pair;          // folded step: 64-row kernels take XCD-paired tiles (tile64)
@@ -859,7 +862,7 @@ struct RedArgsN {
   tt_state* loss_state;
   int32_t apply_adam;
   float* p; float* m; float* v;
-  float lr, b1, b2, eps;
+  double lr, b1, b2, eps;
   AdamSlot* adam_slots;  // non-null: coefficients from slot t & 1; segment next_seg fills t + 1's
   int32_t next_seg;
   tt_state* state;

@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void k_det_scatter(StepArgs a) {  // (round-3 
 
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ P, const float* __restrict__ G,
                                               float* __restrict__ M, float* __restrict__ V, int64_t n,
-                                              float lr, float b1, float b2, float eps, tt_state* state,
+                                              double lr, double b1, double b2, double eps, tt_state* state,
                                               int64_t step_host) {
   const int64_t t = state ? state->step_cur : step_host;
   const AdamCoef c = adam_coef(lr, b1, b2, eps, t);

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TT_ABI_VERSION 4
+#define TT_ABI_VERSION 5
 #define TT_MAX_CAT 16      /* categorical columns per tower */
 
 /* status codes */
@@ -103,9 +103,13 @@ typedef struct tt_batch {
   int64_t t_base;
 } tt_batch;
 
-/* torch.optim.Adam defaults used by train_model (training.py:32) */
+/* torch.optim.Adam hyperparameters of train_model (training.py:32), as the
+ * reference passes them: Python floats (double).  The coefficients follow
+ * torch's _single_tensor_adam from these doubles (bias corrections in
+ * double, each scalar cast to float where torch casts it), so a fused step
+ * equals torch.optim.Adam applied to the same fp32 gradient. */
 typedef struct tt_adam_hp {
-  float lr, beta1, beta2, eps;
+  double lr, beta1, beta2, eps;
 } tt_adam_hp;
 
 /* Device-resident step counters (so a captured hipGraph can be replayed). */

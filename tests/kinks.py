@@ -93,3 +93,49 @@ def adam1_bounds(O, P, lo: Dict[str, torch.Tensor], hi: Dict[str, torch.Tensor],
         outs.append(Pc)
     a, b = outs
     return {k: torch.minimum(a[k], b[k]) for k in a}, {k: torch.maximum(a[k], b[k]) for k in a}
+
+
+def adam1_replay_error(p0, g, p1, m1, v1, lr: float, m0=None, v0=None, t: int = 1, detail: bool = False):
+    """The fused state after ONE Adam step against torch.optim.Adam
+    (single-tensor, fp32, on the CPU) applied to the fused step's OWN
+    gradient ``g`` from the same parameters ``p0``.  The gradient itself is
+    held to the fp64 oracle by ``bound_error``; this pins the optimizer
+    arithmetic element by element, which the parameter box of
+    ``adam1_bounds`` cannot (a first Adam step is g / (|g| + eps): near-zero
+    components may move by anything up to +-lr there).  Returns the largest
+    deviation in units of 2 ulp of each element (of its terms' magnitude
+    for exp_avg, whose terms may cancel; + 1e-6 lr for the parameters) --
+    < 1 passes;
+    the kernel's fp32 sequence is torch's, up to an FMA contraction (1 ulp
+    of exp_avg_sq).  ``m0``, ``v0``, ``t``: the moments before step t > 1."""
+    P = torch.as_tensor(np.asarray(p0, np.float32)).clone()
+    P.grad = torch.as_tensor(np.asarray(g, np.float32)).clone()
+    opt = torch.optim.Adam([P], lr=lr, foreach=False, fused=False)
+    if t > 1:
+        opt.state[P] = {"step": torch.tensor(float(t - 1)),
+                        "exp_avg": torch.as_tensor(np.asarray(m0, np.float32)).clone().view_as(P),
+                        "exp_avg_sq": torch.as_tensor(np.asarray(v0, np.float32)).clone().view_as(P)}
+    opt.step()
+    st = opt.state[P]
+    worst, info = 0.0, None
+    # the magnitude each result is rounded at: exp_avg = b1 m0 + (1 - b1) g
+    # may cancel far below its terms (torch's CPU lerp and the kernel's may
+    # round the terms differently: FMA or not), so its ulp is the terms'
+    gv = np.abs(np.asarray(g, np.float64).reshape(-1))
+    m_mag = 0.1 * gv + (0.9 * np.abs(np.asarray(m0, np.float64).reshape(-1)) if t > 1 else 0.0)
+    for name, got, want, mag, floor in (("p", p1, P.detach(), None, 1e-6 * lr),
+                                        ("exp_avg", m1, st["exp_avg"], m_mag, 1e-38),
+                                        ("exp_avg_sq", v1, st["exp_avg_sq"], None, 1e-38)):
+        got = np.asarray(got, np.float32).reshape(-1).astype(np.float64)
+        want = want.numpy().reshape(-1)
+        mag = np.abs(want).astype(np.float64) if mag is None else np.maximum(mag, np.abs(want))
+        tol = 2.0 * np.spacing(mag.astype(np.float32)).astype(np.float64) + floor
+        if got.size:
+            r = np.abs(got - want.astype(np.float64)) / tol
+            i = int(np.argmax(r))
+            if r[i] > worst:
+                worst = float(r[i])
+                gi = np.asarray(g, np.float32).reshape(-1)[i]
+                info = (name, i, float(got[i]), float(want[i]), float(gi),
+                        float(np.asarray(p0, np.float32).reshape(-1)[i]))
+    return (worst, info) if detail else worst

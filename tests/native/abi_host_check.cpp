@@ -86,7 +86,7 @@ int main() {
     CHECK(tt_forward(&d, nullptr, p, nbt, &bt, 1, 0, 1, p, 1 << 30, p, nullptr) == TT_ERR_ARG);
     CHECK(tt_forward(&d, p, p, nbt, nullptr, 1, 0, 1, p, 1 << 30, p, nullptr) == TT_ERR_ARG);
     CHECK(tt_backward_ex(&d, p, nullptr, &bt, p, 0, 0, 1, p, 1 << 30, p, nullptr, nullptr, nullptr) == TT_ERR_ARG);
-    tt_adam_hp hp = {4e-4f, 0.9f, 0.999f, 1e-8f};
+    tt_adam_hp hp = {4e-4, 0.9, 0.999, 1e-8};
     CHECK(tt_train_step(&d, p, p, nbt, &bt, &hp, 0, nullptr, p, 1 << 30, p, p, p, 1, nullptr) == TT_ERR_ARG);
     CHECK(tt_adam_apply(p, p, p, p, -1, &hp, nullptr, 1, nullptr) == TT_ERR_ARG);
     tt_batch nob = bt;
@@ -107,7 +107,7 @@ int main() {
     bt.num[0] = bt.num[1] = p;
     bt.num_ld[0] = bt.num_ld[1] = 64;
     int64_t nbt[4] = {0, 0, 0, 0};
-    tt_adam_hp hp = {4e-4f, 0.9f, 0.999f, 1e-8f};
+    tt_adam_hp hp = {4e-4, 0.9, 0.999, 1e-8};
     const int64_t ws = tt_workspace_bytes(&d, 16384);
     (void)tt_train_flush(&d, p, p, nbt, &bt, &hp, reinterpret_cast<tt_state*>(p), p, ws, p, p, p, nullptr);
     d.flags |= TT_FLAG_DEFER_LATE | TT_FLAG_LATE_PENDING;

@@ -60,7 +60,7 @@ def test_struct_sizes_match_header_layout():
     assert ctypes.sizeof(N.TTModelDesc) == 4 * (7 + 2 * N.TT_MAX_CAT + 3 + 1)
     assert header_define("TT_FLAG_DETERMINISTIC") == N.TT_FLAG_DETERMINISTIC
     assert ctypes.sizeof(N.TTBatch) == 8 * 15
-    assert ctypes.sizeof(N.TTAdamHP) == 16
+    assert ctypes.sizeof(N.TTAdamHP) == 32
 
 
 def _model(case):

@@ -22,7 +22,7 @@ import torch
 import torch.multiprocessing as mp
 
 from conftest import excluded_param, load_golden, meta_of, sub
-from kinks import adam1_bounds, bound_error, grad_bounds, kink_elements
+from kinks import adam1_bounds, adam1_replay_error, bound_error, grad_bounds, kink_elements
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -78,9 +78,9 @@ def _rank(rank, world, port, q, exchange):
         allp = [None] * world
         dist.all_gather_object(allp, flat.tobytes())
         q.put((rank, tr.grad.cpu().numpy().copy(), flat, all(a == allp[0] for a in allp), loss,
-               tr.steps_done()))
+               tr.steps_done(), tr.exp_avg.cpu().numpy().copy(), tr.exp_avg_sq.cpu().numpy().copy()))
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, repr(e), None, False, None, None))
+        q.put((rank, repr(e), None, False, None, None, None, None))
         raise
     finally:
         dist.destroy_process_group()
@@ -152,7 +152,9 @@ def test_cfg4_eight_ranks_one_step_vs_oracle_ddp(exchange):
     assert all(p.exitcode == 0 for p in ps), [(p.exitcode, r[1] if isinstance(r[1], str) else "") for p, r in
                                               zip(ps, res)]
     slots = _slots(meta)
-    for rank, grad, params, same, loss, steps in res:
+    g = load_golden("cfg3")
+    init = {k: np.asarray(v, np.float32) for k, v in sub(g, "init").items()}
+    for rank, grad, params, same, loss, steps, m1, v1 in res:
         assert same is True, rank
         assert steps == 1
         assert abs(loss - losses[rank]) <= TOL * abs(losses[rank]), (rank, loss, losses[rank])
@@ -164,3 +166,8 @@ def test_cfg4_eight_ranks_one_step_vs_oracle_ddp(exchange):
             assert eg < TOL, ("grad", rank, name, eg, n_kinks)
             ep = bound_error(params[off:off + n], plo[name].numpy(), phi[name].numpy(), plo[name].numpy())
             assert ep < TOL, ("param", rank, name, ep, n_kinks)
+        for name, shape, off in slots:  # Adam on the exchanged mean gradient, element by element
+            n = int(np.prod(shape)) if len(shape) else 1
+            sl = slice(off, off + n)
+            ea = adam1_replay_error(init[name].reshape(-1), grad[sl], params[sl], m1[sl], v1[sl], 4e-4)
+            assert ea < 1.0, ("adam replay", rank, name, ea)

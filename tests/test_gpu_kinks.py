@@ -22,7 +22,7 @@ import pytest
 import torch
 
 from conftest import excluded_param, load_golden, meta_of, normwise, sub
-from kinks import adam1_bounds, bound_error, grad_bounds, kink_elements
+from kinks import adam1_bounds, adam1_replay_error, bound_error, grad_bounds, kink_elements
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -82,6 +82,26 @@ def _grad_of(m, tr, name):
     prm = dict(m.named_parameters())[name]
     off = (prm.data_ptr() - base) // 4
     return tr.grad[off:off + prm.numel()].view(prm.shape).cpu().double().numpy()
+
+
+def _state_of(tr, m, name, which):
+    """the fused trainer's fp32 exp_avg / exp_avg_sq slice of one parameter"""
+    base = tr.arena.params.data_ptr()
+    prm = dict(m.named_parameters())[name]
+    off = (prm.data_ptr() - base) // 4
+    return getattr(tr, which)[off:off + prm.numel()].cpu().numpy()
+
+
+def _check_adam_replay(m, tr, P):
+    """every parameter: the fused Adam step equals torch's Adam applied to
+    the fused gradient (kinks.adam1_replay_error)"""
+    sd = m.state_dict()
+    for n in P:
+        err = adam1_replay_error(P[n].float().numpy(), _grad_of(m, tr, n), sd[n].cpu().numpy(),
+                                 _state_of(tr, m, n, "exp_avg"), _state_of(tr, m, n, "exp_avg_sq"), 4e-4)
+        assert err < 1.0, ("adam replay", n, err, P[n].float().numpy().reshape(-1)[:2], _grad_of(m, tr, n).reshape(-1)[:2],
+                           sd[n].cpu().numpy().reshape(-1)[:2], _state_of(tr, m, n, "exp_avg")[:2],
+                           _state_of(tr, m, n, "exp_avg_sq")[:2])
 
 
 def _zero_columns(P):
@@ -149,6 +169,7 @@ def test_exact_kink_zero_variance_columns(B, p, det):
             assert normwise(sd[k].cpu().numpy(), v.numpy()) < TOL, k
     assert float(sd["firm_tower.1.running_var"][5]) == pytest.approx(0.9, abs=1e-7)
     assert float(sd["ceo_tower.5.running_var"][7]) == pytest.approx(0.9, abs=1e-7)
+    _check_adam_replay(m, tr, P)
 
 
 @pytest.mark.parametrize("det", [False, True], ids=["atomics", "deterministic"])
@@ -188,6 +209,7 @@ def test_unscreened_large_batch_vs_kink_bounds(p, det):
             continue
         err = bound_error(sd[n].cpu().double().numpy(), plo[n].numpy(), phi[n].numpy(), plo[n].numpy())
         assert err < TOL, ("param", n, err, len(elems))
+    _check_adam_replay(m, tr, P)
 
 
 @pytest.mark.parametrize("det", [False, True], ids=["atomics", "deterministic"])
@@ -197,7 +219,9 @@ def test_every_step_gradient_at_the_fused_parameters(det):
     4-step cfg-3 run (B = 16384, dropout 0.1, unscreened data) is held to the
     1e-5 bar on its own: the fused step's gradient against the fp64 oracle's
     gradient AT THE FUSED PARAMETERS of that step (the oracle re-synced to the
-    kernels' trajectory each step), inside the kink bounds."""
+    kernels' trajectory each step), inside the kink bounds; and the step's
+    parameters and moments against torch's Adam applied to that gradient
+    from the step's starting state (kinks.adam1_replay_error)."""
     from ceo_firm_matching import CEOFirmMatcher, Config
     from ceo_firm_matching.engine import FusedTrainer
     from oracle import two_tower as O
@@ -218,8 +242,16 @@ def test_every_step_gradient_at_the_fused_parameters(det):
     names = [n for n, _ in m.named_parameters()]
     for k in range(K):
         P = {n: prm.detach().cpu().double().clone() for n, prm in m.named_parameters()}
+        M0 = {n: _state_of(tr, m, n, "exp_avg") for n in P}
+        V0 = {n: _state_of(tr, m, n, "exp_avg_sq") for n in P}
         tr.step(None, k * B, B)
         torch.cuda.synchronize()
+        sd = m.state_dict()
+        for n in names:  # the optimizer arithmetic of step k + 1 on the fused gradient
+            err, info = adam1_replay_error(P[n].float().numpy(), _grad_of(m, tr, n), sd[n].cpu().numpy(),
+                                           _state_of(tr, m, n, "exp_avg"), _state_of(tr, m, n, "exp_avg_sq"), 4e-4,
+                                           M0[n], V0[n], k + 1, detail=True)
+            assert err < 1.0, ("adam replay", k, n, err, info)
         bk = {n: v[k * B:(k + 1) * B] for n, v in data.items()}
         masks = {(t, l): torch.from_numpy(O.dropout_keep_mask(seed, k + 1, t, l, B, H, p)).double()
                  for t in range(2) for l, H in enumerate((64, 32))}

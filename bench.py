@@ -615,6 +615,9 @@ def main():
     rows = torch.randperm(shard, device=dev, generator=gen)
     if os.environ.get("CEO_BENCH_SEQ_ROWS"):  # diagnostic: in-order rows (gather locality probe)
         rows = torch.arange(shard, device=dev)
+    if os.environ.get("CEO_BENCH_SORT_BATCHES"):  # diagnostic: each batch's rows in index order
+        nb = n_batches * B
+        rows[:nb] = rows[:nb].view(n_batches, B).sort(dim=1).values.reshape(-1)
 
     # hipGraph replay of whole steps at every world size: the RCCL all-reduce
     # of the data-parallel step is captured with the kernels (no host work

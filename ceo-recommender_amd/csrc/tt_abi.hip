@@ -721,7 +721,7 @@ static void launch_first(const StepArgs& a, const Plan& P, hipStream_t s, Evs ev
     launch(k_bwd_first<ROWS>, dim3(P.n_tiles_mid, 2), dim3(4 * ROWS), P.lds_first, s, ev, a);
 }
 static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}, bool ex = false) {
-  const dim3 grid((unsigned)(r.vn / RED_E + r.pf_blocks)), blk(RED_E * RED_G);
+  const dim3 grid((unsigned)(r.vn / RED_E)), blk(RED_E * RED_G);
   if (ex)  // data-parallel exchange inside the reduction (tt_train_step_dp: Adam slots set)
     launch(k_reduce_adam<true, true>, grid, blk, 0, s, ev, r);
   else if (r.adam_slots || !r.apply_adam)  // <true> reads no coefficients when there is no Adam
@@ -1118,23 +1118,6 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   det_fold(a, c.P, DET_FIRST, s);
   red_step_fields(r, defer ? RED_EARLY : RED_ALL, c.W, w, b->n_rows, state, apply_adam, params, exp_avg,
                   exp_avg_sq, hp, a.adam_slots);
-#if TT_PREFETCH_NEXT
-  // single-GPU cycle-mode steps of numeric towers: the next step's rows are
-  // known on the device (the step counter), prefetch them
-  if (!x && b->cycle > 0 && c.L.n_num[0] > 0 && c.L.n_num[1] > 0) {
-    for (int t = 0; t < 2; ++t) {
-      r.pf_num[t] = (const float*)b->num[t];
-      r.pf_ld[t] = b->num_ld[t];
-      r.pf_cols[t] = c.L.n_num[t];
-    }
-    r.pf_rows = (const int64_t*)b->rows;
-    r.pf_B = b->n_rows;
-    r.pf_cycle = b->cycle;
-    r.pf_tbase = b->t_base;
-    r.pf_blocks = (int32_t)((b->n_rows + 255) / 256);
-    r.pf_sink = w + c.W.late + 8;
-  }
-#endif
   launch_reduce(r, s, ev(5), x != nullptr);
   return launch_check();
 }

@@ -43,18 +43,6 @@ constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 #ifndef TT_BWD32_MAX_B
 #define TT_BWD32_MAX_B 0  // (off: measured slower) unfolded batches below it run k_bwd_mid / k_bwd_first on 32-row blocks
 #endif
-#ifndef TT_L4_SHIFT_ALL
-#define TT_L4_SHIFT_ALL 0  // k_l4_fwd: every wave computes both BN1 shift tiles (no LDS hand-off / barrier)
-#endif
-#ifndef TT_PREFETCH_NEXT
-#define TT_PREFETCH_NEXT 0  // k_reduce_adam prefetches the next step's batch rows (Infinity Cache)
-#endif
-#ifndef TT_FOLD_REP_FIRST
-#define TT_FOLD_REP_FIRST 0  // k_bwd_mid_fold: BN1-affine replica loads issued first (RepSum1)
-#endif
-#ifndef TT_PAIR_REP_FIRST
-#define TT_PAIR_REP_FIRST 0  // k_top_pair: BN1 moment replica loads issued first
-#endif
 #ifndef TT_FOLD_MIN_B
 #define TT_FOLD_MIN_B 4096  // smallest batch that runs the folded BN0 backward (round 5: cfg 2 40.0 -> 38.9 us)
 #endif
@@ -876,17 +864,6 @@ struct RedArgsN {
   // step_cur meanwhile)
   int64_t* late_pending;
   int32_t late_mark;     // early half: 1 records t + 1 (deferring), -1 records 0 (not deferring), 0 leaves it
-  // TT_PREFETCH_NEXT (k_reduce_adam of a cycle-mode step): pf_blocks extra
-  // blocks after the element blocks touch every 128-B line of the NEXT step's
-  // batch rows of both towers' numeric features, so k_l0_fwd(t + 1) gathers
-  // them from the Infinity Cache instead of HBM
-  const float* pf_num[2];
-  int64_t pf_ld[2];
-  int32_t pf_cols[2];
-  const int64_t* pf_rows;
-  int64_t pf_B, pf_cycle, pf_tbase;
-  int32_t pf_blocks;
-  float* pf_sink;        // never written for finite data (keeps the loads alive)
 };
 using RedArgs = RedArgsN<MAX_SEG>;
 constexpr int MAX_LATE_SEG = 8;

@@ -79,9 +79,6 @@ using CfgSim = Cfg<256, 128, 64>;
 using CfgSim = Cfg<256, 256, 128>;
 #endif
 using CfgGrad = Cfg<256, 256, 128>;
-#ifndef TT_NCE_NOSPLIT_PROBE
-#define TT_NCE_NOSPLIT_PROBE 0
-#endif
 #ifndef TT_NCE_PIPE
 // the similarity kernels' gemm_loop reads B fragments one tile ahead of the
 // MFMAs (cfg 5: fwd 28.2 -> 27.9 ms, ranks 23.9 -> 23.6 ms); the gradient
@@ -340,16 +337,7 @@ __device__ __forceinline__ void store_opnd(uint16_t* L, const float4 (&v)[ROWS *
       const float x[8] = {v[2 * t].x,     v[2 * t].y,     v[2 * t].z,     v[2 * t].w,
                           v[2 * t + 1].x, v[2 * t + 1].y, v[2 * t + 1].z, v[2 * t + 1].w};
       bf16x8 pl[NPL];
-#if TT_NCE_NOSPLIT_PROBE  // timing probe only: wrong planes, no split VALU
-      {
-        u32x4 h;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) h[q] = __builtin_amdgcn_perm(__float_as_uint(x[2 * q + 1]), __float_as_uint(x[2 * q]), 0x07060302u);
-        pl[0] = pl[1] = pl[2] = __builtin_bit_cast(bf16x8, h);
-      }
-#else
       split8x3(x, pl);
-#endif
       uint16_t* d = L + lds_off<SWZ>(m, k8);
       *reinterpret_cast<bf16x8*>(d) = pl[0];
       *reinterpret_cast<bf16x8*>(d + PLANE) = pl[1];

@@ -28,36 +28,11 @@ namespace tt {
 // reads 64 B of one 128-B P|Q row segment.
 // PRE: the step's Adam coefficients come from the workspace cache (AdamSlot,
 // tt_common.h: a fused train step); otherwise the owner lanes compute them.
-// The next step's batch rows (cycle mode: row0 = ((t - t_base) % cycle) B for
-// step t + 1) touched line by line: two threads per row, each tower's 128-B
-// line `line` of the row, the row index loaded first.  The sum of the loaded
-// values is compared with a bit pattern no finite input has, so the loads
-// stay; nothing is written for finite data.
-__device__ __forceinline__ void prefetch_next_rows(const RedArgs& a, int pb) {
-  if (a.pf_cycle <= 0) return;
-  const int64_t t = a.state ? a.state->step_cur : a.step_host;
-  const int64_t base = ((t - a.pf_tbase) % a.pf_cycle) * a.pf_B;
-  const int64_t rpb = (a.pf_B + a.pf_blocks - 1) / a.pf_blocks;
-  const int64_t i = min((int64_t)pb * rpb + (threadIdx.x >> 1), a.pf_B - 1);
-  const int line = threadIdx.x & 1;
-  const int64_t drow = a.pf_rows ? a.pf_rows[base + i] : base + i;
-  const float v0 = a.pf_num[0][drow * a.pf_ld[0] + min(32 * line, a.pf_cols[0] - 1)];
-  const float v1 = a.pf_num[1][drow * a.pf_ld[1] + min(32 * line, a.pf_cols[1] - 1)];
-  if (__float_as_uint(v0) == 0xFFFFFFFFu && __float_as_uint(v1) == 0xFFFFFFFFu) *a.pf_sink = v0 + v1;
-}
-
 template <bool PRE, bool EX>
 __global__ __launch_bounds__(RED_E* RED_G, TT_RED_MINW) void k_reduce_adam(RedArgs a) {
   __shared__ float part[RED_G * RED_E];
   __shared__ float xpart[4 * RED_G * RED_E];  // kinds 3, 4: gg0, gbe0, sum Zh0, sum X' replicas
   __shared__ int xok_s;
-#if TT_PREFETCH_NEXT
-  const int nb = (int)(a.vn / RED_E);
-  if ((int)blockIdx.x >= nb) {  // (whole block: uniform)
-    prefetch_next_rows(a, (int)blockIdx.x - nb);
-    return;
-  }
-#endif
   reduce_body<RedArgs, RED_G, PRE, EX, false>(a, (int)blockIdx.x, part, xpart, &xok_s);
 }
 

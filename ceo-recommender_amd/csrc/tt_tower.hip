@@ -697,45 +697,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
 
   // ---- Z4 = A0 W4^T (bf16x3, two K steps per 16-column tile); waves 0 and 1
   // also compute tile w of the shift row with the same MFMA sequence in every
-  // block (bitwise one shift for all blocks).  TT_L4_SHIFT_ALL: every wave
-  // computes both shift tiles itself (its lanes' columns r and 16 + r), so
-  // no LDS hand-off and no barrier
-#if TT_L4_SHIFT_ALL
-  f32x4 acc[2] = {zero4(), zero4()}, accs2[2] = {zero4(), zero4()};
-  {
-    bf16x8 sa[2][3];
-    if (a.train) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const f32x4* ap = reinterpret_cast<const f32x4*>(a0r + 32 * kk + 8 * g);
-        const f32x4 p0 = ap[0], p1 = ap[1];
-        const float xs[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
-        split8x3(xs, sa[kk]);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        bf16x8 wf[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          wf[p] = *reinterpret_cast<const bf16x8*>(Wh + p * PL + (16 * j + r) * LDK + 32 * kk + 8 * g);
-        mfma_x3(xa[kk], wf, acc[j]);
-        if (a.train) mfma_x3(sa[kk], wf, accs2[j]);
-      }
-    }
-  }
-  float shv[2] = {0.f, 0.f};
-  if (a.train) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      shv[j] = accs2[j][0] + bias[j];
-      if (blockIdx.x == 0 && w == 0 && g == 0) T.shift1[16 * j + r] = shv[j];
-    }
-  }
-  (void)shl;
-#else
+  // block (bitwise one shift for all blocks)
   f32x4 acc[2] = {zero4(), zero4()}, accs = zero4();
   {
     bf16x8 sa[2][3];
@@ -778,17 +740,12 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     }
     __syncthreads();  // shl
   }
-#endif
   TT_STAMP(1, 3);
 
   float s1[2], s2[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-#if TT_L4_SHIFT_ALL
-    const float sh = shv[j];
-#else
     const float sh = a.train ? shl[16 * j + r] : 0.f;
-#endif
     s1[j] = 0.f;
     s2[j] = 0.f;
 #pragma unroll
@@ -1349,12 +1306,6 @@ __global__ __launch_bounds__(R * 8) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs 
 
   // ---- phase 0: every load -- own tower's Z4 slice, both W8 (raw), biases,
   // logit_scale, (target, weight), BN1 inputs, BN1 moment replicas
-  // (TT_PAIR_REP_FIRST: the replicas first, so their sum and the coefficient
-  // chain wait for them alone)
-#if TT_PAIR_REP_FIRST
-  RepSum2<NTH, 2 * H1> rs;
-  rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
-#endif
   float4 zs[2];
   {
     const float4* ps_ = reinterpret_cast<const float4*>(T.Z4 + row * H1 + 8 * g);
@@ -1383,10 +1334,8 @@ __global__ __launch_bounds__(R * 8) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs 
     bn_g = g1p[bc];
     bn_be = pick(bt, a.tw[0].be1, a.tw[1].be1)[bc];
   }
-#if !TT_PAIR_REP_FIRST
   RepSum2<NTH, 2 * H1> rs;
   rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
-#endif
   if (threadIdx.x < 2 * DP) smem[L::b8s + threadIdx.x] = (threadIdx.x % DP) < (unsigned)D ? b8v : 0.f;
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {
@@ -1901,12 +1850,6 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
   // ---- phase 0: issue every load -- dY1, Z4, Z0 of this wave's rows (C
   // layout), W4, BN inputs, then (after the step load they depend on) the
   // dataset rows of this thread's X' gather rows and of the shift row.
-  // TT_FOLD_REP_FIRST: the BN1-affine replicas first, so their sum and the
-  // coefficient chain wait for them alone (vmcnt retires in issue order)
-#if TT_FOLD_REP_FIRST
-  RepSum1<NTH, 2 * H1> rs1;
-  rs1.issue(T.gg1, BNG);
-#endif
   f32x4 dy1[2], zz4[2], zz0[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1940,11 +1883,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
 #pragma unroll
   for (int k = 0; k < XK; ++k) xrow[k] = data_row_nb(a, base, min(r0 + xr0 + k, a.B - 1));
   const int64_t crow = data_row_nb(a, base, 0);
-#if TT_FOLD_REP_FIRST
-  rs1.finish(smem + L::rsc, smem + L::rst);
-#else
   rep_sum<NTH, 2 * H1>(T.gg1, BNG, smem + L::rsc, smem + L::rst);  // gg1|gbe1 are adjacent in a replica
-#endif
   {
     const float* rst = smem + L::rst;
     if (threadIdx.x < H1) {

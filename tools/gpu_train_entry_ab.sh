@@ -1,4 +1,4 @@
-# A/B of train()'s rate (bench's train_entry leg): order staging on / off, interleaved
+# A/B of train()'s rate (bench's train_entry leg) under CEO_TT_STAGE_ORDER=1 / 0 (the staging knob measured in round 5 was removed)
 set -o pipefail
 mkdir -p gpurun_out/tab
 timeout -k 10 300 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 200 --timeout-method thread > gpurun_out/tab/pytest.log 2>&1 || { tail -20 gpurun_out/tab/pytest.log; exit 1; }

@@ -607,6 +607,8 @@ def main():
     cfg = Config()
     cfg.LATENT_DIM = D
     cfg.DEVICE = dev
+    if os.environ.get("CEO_BENCH_DROPOUT"):  # diagnostic: the dropout-mask cost (the workload is p = 0.1)
+        cfg.DROPOUT_P = float(os.environ["CEO_BENCH_DROPOUT"])
     torch.manual_seed(42)  # identical init on every rank (DDP broadcast semantics)
     model = CEOFirmMatcher(meta, cfg).to(dev)
     tr = FusedTrainer(model, lr=cfg.LEARNING_RATE, max_batch=B, seed=42, process_group=pg,

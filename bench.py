@@ -127,6 +127,22 @@ def _pmc_kernels():
         return {}
 
 
+def pmc_traffic_stale():
+    """Whether profiles/pmc_traffic.json was measured on another build than
+    the library this process loaded (its library_sha256 stamp, written by
+    tools/pmc_traffic.py; a summary without a stamp counts as stale)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as fh:
+            stamp = json.load(fh).get("library_sha256")
+        import hashlib
+        from ceo_firm_matching import _native as N
+        with open(N.LIB_PATH, "rb") as fh:
+            return stamp != hashlib.sha256(fh.read()).hexdigest()
+    except Exception:
+        return True
+
+
 def load_pmc_traffic(name):
     """HBM bytes per launch from a committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json written by tools/pmc_traffic.py), or None."""
@@ -877,6 +893,7 @@ def run_extras(args, result, dev, pg, world, rank, held, B, n_batches, elapsed, 
     roof["kernel"] = dom
     roof["avg_us"] = round(per[dom], 3)
     roof["traffic"] = load_pmc_traffic(dom)
+    roof["traffic_stale"] = pmc_traffic_stale()
     result["roofline"] = roof
     # the whole step against the same peaks: reference FLOPs per pair x B
     # over the timed ms_per_step, and the PMC bytes of all the step's

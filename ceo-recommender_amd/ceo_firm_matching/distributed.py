@@ -86,14 +86,85 @@ def agree_exchange_form(ok: bool, t_fused_us: float, t_two_us: float, group=None
     rank's reduce -> exchange + Adam step.  Returns (use_fused, (fused_us,
     two_launch_us)) with the MAX-over-ranks times (inf where not measured).
     ``prefer_fused`` (CEO_TT_FUSED_EX=1, tests): the bitwise check alone decides."""
-    bad = 0.0 if ok else 1.0
-    if group is not None and dist.is_available() and dist.is_initialized():
-        dev = device if dist.get_backend(group) == "nccl" else "cpu"
-        v = torch.tensor([bad, float(t_fused_us), float(t_two_us)], dtype=torch.float64, device=dev)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
-        bad, t_fused_us, t_two_us = (float(x) for x in v.cpu())
+    bad, t_fused_us, t_two_us = _max_over_ranks([0.0 if ok else 1.0, t_fused_us, t_two_us], group, device)
     use = bad == 0.0 and (prefer_fused or t_fused_us <= t_two_us)
     return use, (round(t_fused_us, 2), round(t_two_us, 2))
+
+
+def _max_over_ranks(values, group=None, device=None):
+    """Element-wise MAX over the ranks of ``group`` of a list of floats (the
+    list itself without a process group)."""
+    vals = [float(x) for x in values]
+    if group is not None and dist.is_available() and dist.is_initialized():
+        dev = device if dist.get_backend(group) == "nccl" else "cpu"
+        v = torch.tensor(vals, dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+        vals = [float(x) for x in v.cpu()]
+    return vals
+
+
+def choose_exchange_form(reference, candidates, restore, group=None, device=None, prefer=None,
+                         before_timing=None):
+    """Pick the data-parallel exchange form on this job's topology, the same
+    choice on every rank (engine.FusedTrainer._validate_fused_exchange).
+
+    ``reference`` and every entry of ``candidates`` are ``(name, run, time)``:
+    ``run()`` does one step from the saved state and returns its result
+    (parameters, moments, buffers, gradient) or None when the form refused or
+    failed; ``time()`` returns device microseconds per step.  ``reference``
+    is the reduce -> exchange + Adam form (itself checked against the
+    collective by ``PeerExchange.create``), the fallback.  A candidate is
+    eligible only if its result is bitwise the reference's on EVERY rank; the
+    eligible forms and the reference are then timed, and the fastest
+    eligible candidate whose MAX-over-ranks time is not above the reference's
+    wins (``prefer``: that candidate wins whenever it is eligible).
+
+    Every rank runs the same collectives in the same order whatever its local
+    outcome: a run or timing that raises counts as a failure of that form on
+    that rank (never an exception out of here, which would leave the other
+    ranks waiting in ``restore`` or in an agreement), the eligibility is
+    agreed before any rank times anything, and ``restore()`` -- a collective
+    that puts the saved state back -- follows every run and every timing.
+    Returns (chosen name, {name: MAX-over-ranks us, inf where not timed})."""
+    import math
+    import warnings
+
+    def guard(fn, what):
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- a failed form, decided jointly below
+            warnings.warn(f"exchange form {what}: {type(e).__name__}: {e}")
+            return None
+
+    ref_name, ref_run, ref_time = reference
+    ref = guard(ref_run, ref_name)
+    restore()
+    bad = []
+    for name, run, _ in candidates:
+        out = guard(run, name)
+        restore()
+        bad.append(0.0 if (ref is not None and out is not None and torch.equal(out, ref)) else 1.0)
+    bad = _max_over_ranks([0.0 if ref is not None else 1.0] + bad, group, device)
+    eligible = [bad[0] == 0.0 and b == 0.0 for b in bad[1:]]
+    if before_timing is not None:
+        before_timing()
+    local = []
+    for (name, _, time_fn), go in zip([reference] + list(candidates), [True] + eligible):
+        t = guard(time_fn, name) if go else None
+        if go:
+            restore()
+        local.append(math.inf if t is None else float(t))
+    times = _max_over_ranks(local, group, device)
+    out_t = {n: round(t, 2) for (n, _, _), t in zip([reference] + list(candidates), times)}
+    best, best_t = ref_name, times[0]
+    for (name, _, _), go, t in zip(candidates, eligible, times[1:]):
+        if not go:
+            continue
+        if name == prefer:
+            return name, out_t
+        if t <= best_t:
+            best, best_t = name, t
+    return best, out_t
 
 
 def broadcast_state_(params: torch.Tensor, buffers: Optional[torch.Tensor] = None, group=None, src: int = 0):

@@ -17,13 +17,12 @@ flat fp32 gradient is all-reduced (AVG, one call per step), and
 """
 from __future__ import annotations
 
-import weakref
 from typing import Dict, Optional
 
 import torch
 
 from . import _native as N
-from .distributed import PeerExchange, agree_exchange_form, average_gradients_, broadcast_state_, world_of
+from .distributed import PeerExchange, average_gradients_, broadcast_state_, choose_exchange_form, world_of
 from .model import CEOFirmMatcher, check_category_codes
 
 DATA_KEYS = ("firm_numeric", "firm_cat", "ceo_numeric", "ceo_cat", "target", "weights")
@@ -77,6 +76,7 @@ class FusedTrainer:
         # (fused, two-launch) device us per step, MAX over ranks, measured by
         # _validate_fused_exchange on the first data-parallel step
         self.fused_vs_two_launch_us = None
+        self.exchange_form_us = None  # {form: us}, all forms timed by the validation
         # TT_FLAG_DEFER_LATE: each single-GPU step leaves the late half of its
         # reduction (W4, BN1 affine, W8, logit_scale, the loss) to the next
         # step's first kernel; flush() finishes it (run automatically before
@@ -165,7 +165,10 @@ class FusedTrainer:
         N.check(rc, "tt_train_step", n_rows, 64)
         if defer:
             self._late_rows, self._late_batch = n_rows, batch
-            self.model._pending_flush = weakref.WeakMethod(self.flush)
+            # a strong reference while (only while) a late half is pending: a
+            # trainer dropped now is kept alive by the model until that late
+            # half has run (sync_trainer), so the update is never lost
+            self.model._pending_flush = self.flush
         elif self._late_rows:  # (consumed by this step's first kernel)
             self._late_rows, self._late_batch = 0, None
             self.model._pending_flush = None
@@ -196,7 +199,7 @@ class FusedTrainer:
         last replayed step's late half.  The device guard makes a flush of
         nothing a no-op, never a second late half."""
         self._late_rows, self._late_batch = state
-        self.model._pending_flush = weakref.WeakMethod(self.flush) if state[0] else None
+        self.model._pending_flush = self.flush if state[0] else None
 
     def _launch_dp(self, batch, n_rows):
         """The data-parallel step: the exchange inside the step's reduction
@@ -227,8 +230,10 @@ class FusedTrainer:
         keep the fused form only if every rank finished both without a
         timeout and got bitwise the same parameters, Adam moments, BN buffers
         and gradient.  The state is restored (and the exchange regions reset)
-        afterwards, so the real step runs from where it started."""
-        import torch.distributed as dist
+        afterwards, so the real step runs from where it started.  The
+        protocol (distributed.choose_exchange_form) runs the same collectives
+        on every rank whatever each rank's outcome, so a rank whose check or
+        timing fails cannot leave its peers waiting."""
         a = self.arena
         live = (a.params, a.buffers, a.nbt, self.grad, self.exp_avg, self.exp_avg_sq, self.state)
         saved = [t.clone() for t in live]
@@ -245,50 +250,55 @@ class FusedTrainer:
 
         def result():
             torch.cuda.synchronize(self.device)
+            if self.peer.failed():
+                return None
             return torch.cat([a.params, self.exp_avg, self.exp_avg_sq, a.buffers, self.grad]).clone()
-        prev_det = self.deterministic
-        self.deterministic = True
-        N.set_deterministic(self.desc, True)
-        t_fused = t_two = float("inf")
-        try:
-            rc = self.peer.train_step(self, batch)
-            ok = rc == N.TT_OK
-            fused = result() if ok else None
-            ok = ok and not self.peer.failed()
-            restore()
+
+        def fused_step():
+            N.check(self.peer.train_step(self, batch), "tt_train_step_dp")
+
+        def two_launch():
             self._launch(batch, n_rows, False)
             self.allreduce_and_adam()
-            two = result()
-            ok = ok and not self.peer.failed() and torch.equal(fused, two)
-            restore()
-            # then by speed, in the mode the steps will run in: k steps of
-            # each form from the saved state (state restored after each)
-            self.deterministic = prev_det
-            N.set_deterministic(self.desc, self.is_deterministic())
-            if ok:
-                t_fused = self._time_steps(lambda: self.peer.train_step(self, batch))
-                ok = not self.peer.failed()
-                restore()
 
-                def two_launch():
-                    self._launch(batch, n_rows, False)
-                    self.allreduce_and_adam()
-                t_two = self._time_steps(two_launch)
-                ok = ok and not self.peer.failed()
-                restore()
-        finally:
+        def run(fn):
+            def go():
+                fn()
+                return result()
+            return go
+
+        def timed(fn):
+            def go():
+                t = self._time_steps(fn)
+                if self.peer.failed():
+                    raise RuntimeError("an exchange timed out while timing")
+                return t
+            return go
+
+        prev_det = self.deterministic
+
+        def steps_mode():  # time in the mode the steps will run in
             self.deterministic = prev_det
             N.set_deterministic(self.desc, self.is_deterministic())
+        self.deterministic = True  # the bitwise check in deterministic mode
+        N.set_deterministic(self.desc, True)
         import os
-        use, times = agree_exchange_form(ok, t_fused, t_two, self.pg, self.device,
-                                         prefer_fused=os.environ.get("CEO_TT_FUSED_EX") == "1")
-        self.fused_vs_two_launch_us = times
-        return use
+        try:
+            use, times = choose_exchange_form(
+                ("two_launch", run(two_launch), timed(two_launch)),
+                [("fused", run(fused_step), timed(fused_step))], restore, self.pg, self.device,
+                prefer="fused" if os.environ.get("CEO_TT_FUSED_EX") == "1" else None, before_timing=steps_mode)
+        finally:
+            steps_mode()
+        self.exchange_form_us = times
+        self.fused_vs_two_launch_us = (times["fused"], times["two_launch"])
+        return use == "fused"
 
     def _time_steps(self, fn, k: int = 8) -> float:
         """Device time per step (us) of k back-to-back calls of ``fn``: the
         launches queue behind a short GPU spin so the events bracket the
-        kernels, not the host's enqueue rate."""
+        kernels, not the host's enqueue rate.  Collective: every rank calls it
+        (a barrier first)."""
         import torch.distributed as dist
         torch.cuda.synchronize(self.device)
         if self.pg is not None:
@@ -300,9 +310,7 @@ class FusedTrainer:
             pass
         e0.record()
         for _ in range(k):
-            rc = fn()
-            if rc is not None and rc != N.TT_OK:
-                N.check(rc, "exchange timing step")
+            fn()
         e1.record()
         torch.cuda.synchronize(self.device)
         return 1e3 * e0.elapsed_time(e1) / k

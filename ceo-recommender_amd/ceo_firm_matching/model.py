@@ -77,14 +77,13 @@ class CEOFirmMatcher(nn.Module):
 
     def sync_trainer(self):
         """Finish a deferred optimizer step of the training engine, if any.
-        The trainer is held through a weak reference (engine.FusedTrainer
-        registers ``weakref.WeakMethod(trainer.flush)``): the model does not
-        keep a trainer and its workspace alive."""
-        ref = self._pending_flush
-        if ref is not None:
-            fn = ref()
-            if fn is not None:
-                fn()
+        engine.FusedTrainer registers its bound ``flush`` here only while a
+        late half is pending (a strong reference: a trainer dropped with a
+        pending step stays alive until the step is finished here, never losing
+        it) and clears it once the late half has run."""
+        fn = self._pending_flush
+        if fn is not None:
+            fn()
             self._pending_flush = None
 
     def __getstate__(self):

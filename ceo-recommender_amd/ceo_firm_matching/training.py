@@ -82,18 +82,56 @@ def epoch_order_plan(loader: DataLoader, pin: bool = False) -> Optional[Callable
     return build
 
 
+_RANDPERM_AGREES = None
+
+
+def native_randperm_agrees() -> bool:
+    """Whether tt_randperm (a restatement of torch 2.10's CPU randperm:
+    mt19937 Fisher-Yates) still equals this process's ``torch.randperm``:
+    compared once per process on a few sizes and seeds that cover the small-n
+    and the Fisher-Yates paths.  A torch whose randperm draws otherwise makes
+    host_randperm fall back to torch (with a warning) instead of silently
+    training in another order than the reference's DataLoader."""
+    global _RANDPERM_AGREES
+    if _RANDPERM_AGREES is None:
+        from . import _native as N
+        agree = True
+        try:
+            for n, seed in ((0, 1), (1, 3), (7, 0), (1000, 12345), (70_001, 2 ** 40 + 7)):
+                got = N.randperm(n, seed, False)
+                if got is None:
+                    continue
+                gen = torch.Generator()
+                gen.manual_seed(seed)
+                if not torch.equal(got, torch.randperm(n, generator=gen)):
+                    agree = False
+                    break
+        except N.NativeLibraryError:
+            agree = True  # (host_randperm then uses torch anyway)
+        if not agree:
+            import warnings
+            warnings.warn(f"tt_randperm differs from torch {torch.__version__}'s randperm: "
+                          "epoch orders are drawn with torch.randperm")
+        _RANDPERM_AGREES = agree
+    return _RANDPERM_AGREES
+
+
 def host_randperm(n: int, seed: int, pin: bool = False) -> torch.Tensor:
     """``torch.randperm(n, generator=Generator().manual_seed(seed))``, the
     RandomSampler's draw, built by the library's tt_randperm (the same
     mt19937 Fisher-Yates, bit for bit, with the swap targets prefetched: the
     sequential torch loop is 23 ns per pair, a cache miss per swap); torch's
     own randperm where the library does not cover n or is not built (host
-    work, identical result)."""
+    work, identical result), or where this torch's randperm no longer draws
+    what tt_randperm restates (checked once per process:
+    ``native_randperm_agrees``)."""
     from . import _native as N
-    try:
-        order = N.randperm(n, seed, pin)
-    except N.NativeLibraryError:
-        order = None
+    order = None
+    if native_randperm_agrees():
+        try:
+            order = N.randperm(n, seed, pin)
+        except N.NativeLibraryError:
+            order = None
     if order is None:
         gen = torch.Generator()
         gen.manual_seed(seed)

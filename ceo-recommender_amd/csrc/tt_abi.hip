@@ -444,6 +444,7 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   RedArgs r;
   std::memset(&r, 0, sizeof(r));
   int k = 0;
+  bool overflow = false;
   bool late_range = false;  // set around the late ranges below
   const int G = part == RED_LATE ? LATE_G : RED_G;
   // returns whether the range went into this part's segment list
@@ -451,7 +452,10 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
                  int64_t rep_stride = 0) -> bool {
     if (len <= 0) return false;
     if ((part == RED_EARLY && late_range) || (part == RED_LATE && !late_range)) return false;
-    if (k >= MAX_SEG) std::abort();  // 1 + 2 x 6 + 1 ranges at most (static_assert MAX_SEG >= 14)
+    if (k >= MAX_SEG) {  // 1 + 2 x 6 + 1 ranges at most (static_assert MAX_SEG >= 14)
+      overflow = true;   // reported as n_seg < 0: the caller returns an error before enqueuing
+      return false;
+    }
     r.seg[k].off = off;
     r.seg[k].len = len;
     r.seg[k].kind = kind;
@@ -504,6 +508,10 @@ static RedArgs make_red(const tt_model_desc* d, const Layout& L, const WsLayout&
   late_range = true;
   add(L.ls, 1, 2, 0, 0, 0, ws + W.lsr, LSR);
   late_range = false;
+  if (overflow) {
+    r.n_seg = -1;
+    return r;
+  }
   // element space of k_reduce_adam: every range starts on a block (one
   // segment per block); kind 3 ranges hold every W0 element twice (P and Q
   // halves of one 32-lane group).  Ranges are laid out heaviest first (slab
@@ -991,6 +999,8 @@ static int32_t backward_impl(const tt_model_desc* d, const float* params, const 
     a.drop_thr = 0;
     a.drop_scale = 1.f;
   }
+  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
+  if (r.n_seg < 0) return TT_ERR_UNSUPPORTED;
   (void)hipMemsetAsync(w + c.W.gacc, 0, sizeof(float) * c.L.n, s);
   for (int t = 0; t < 2; ++t) (void)hipMemsetAsync(w + c.W.bng[t], 0, sizeof(float) * NREP * BNG, s);
   (void)hipMemsetAsync(w + c.W.lsr, 0, sizeof(float) * NREP * LSR, s);
@@ -1001,7 +1011,6 @@ static int32_t backward_impl(const tt_model_desc* d, const float* params, const 
   det_fold(a, c.P, DET_MID, s);
   launch_first(a, c.P, s);
   det_fold(a, c.P, DET_FIRST, s);
-  RedArgs r = make_red(d, c.L, c.W, w, c.P, grad);
   r.inv_b = 1.f / (float)b->n_rows;
   launch_reduce(r, s);
   return launch_check();
@@ -1056,6 +1065,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   const bool defer = (d->flags & TT_FLAG_DEFER_LATE) != 0, pending = (d->flags & TT_FLAG_LATE_PENDING) != 0;
   if ((defer || pending) && (!apply_adam || x)) return TT_ERR_UNSUPPORTED;
   RedArgs r = make_red(d, c.L, c.W, w, c.P, grad, defer ? RED_EARLY : RED_ALL);
+  if (r.n_seg < 0) return TT_ERR_UNSUPPORTED;
   r.late_mark = defer ? 1 : -1;
   if (x) {
     // every block of the reduction waits for its peers' same block: all of
@@ -1103,6 +1113,7 @@ static int32_t train_step_impl(const tt_model_desc* d, float* params, float* buf
   LateRed late;
   if (pending) {  // the previous step's late half (same batch size: the caller flushes otherwise)
     RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
+    if (lr.n_seg < 0) return TT_ERR_UNSUPPORTED;
     red_step_fields(lr, RED_LATE, c.W, w, b->n_rows, state, 1, params, exp_avg, exp_avg_sq, hp, a.adam_slots);
     late = to_late(lr);
   }
@@ -1133,6 +1144,7 @@ int32_t tt_train_flush(const tt_model_desc* d, float* params, float* buffers, in
   hipStream_t s = (hipStream_t)stream;
   float* w = (float*)ws;
   RedArgs lr = make_red(d, c.L, c.W, w, c.P, grad, RED_LATE);
+  if (lr.n_seg < 0) return TT_ERR_UNSUPPORTED;
   red_step_fields(lr, RED_LATE, c.W, w, b->n_rows, state, 1, params, exp_avg, exp_avg_sq, hp,
                   reinterpret_cast<AdamSlot*>(w + c.W.adam));
   const LateRed late = to_late(lr);

@@ -231,6 +231,34 @@ def test_workspace_growth_flushes_the_pending_late_half():
         assert ok, (k, normwise(b[k], a[k]), np.max(np.abs(b[k] - a[k])))
 
 
+def test_dropped_trainer_keeps_its_pending_late_half():
+    """A FusedTrainer(defer_late=True) dropped while a late half is pending
+    (ADVICE r05): the model keeps the trainer's flush alive until it reads its
+    parameters, so state_dict() after `del trainer` is the plain run's."""
+    import gc
+    _, _, data, make = _setup(p=0.0)
+    out = []
+    for defer in (False, True):
+        m, tr = make(defer)
+        for k in range(3):
+            tr.step(None, k * B, B)
+        if defer:
+            assert m._pending_flush is not None
+        ref = tr.model  # noqa: F841 -- the model outlives the trainer
+        del tr
+        gc.collect()
+        sd = m.state_dict()
+        assert m._pending_flush is None
+        out.append({k: v.detach().cpu().double().numpy().copy() for k, v in sd.items()})
+    a, b = out
+    for k in a:
+        if excluded_param(k) or "num_batches" in k or "running_mean" in k:
+            continue
+        # a lost late half would leave W4 / W8 / logit_scale a whole Adam step (lr) behind
+        ok = normwise(b[k], a[k]) < 1e-5 or np.max(np.abs(b[k] - a[k])) <= 5e-2 * 4e-4 * 3
+        assert ok, (k, normwise(b[k], a[k]), np.max(np.abs(b[k] - a[k])))
+
+
 def test_deferred_six_kernel_path_cfg2():
     """The cfg-2 geometry (32 x 32 features, LATENT 64, B = 4000: the
     six-kernel path, no folded BN0 backward) deferred vs plain: the same

@@ -65,8 +65,15 @@ def main():
     out_path = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                                    "pmc_traffic.json")
     kernels = traffic(collect(root))
+    # the build the counters describe: bench.py marks roofline.traffic stale
+    # when the library it loaded is another one
+    import hashlib
+    lib = os.environ.get("CEO_TT_LIB") or os.path.join(os.path.dirname(__file__), "..", "ceo-recommender_amd",
+                                                       "lib", "libceo_tt.so")
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
     doc = {
         "source": os.path.basename(os.path.normpath(root)),
+        "library_sha256": sha,
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
                   "bytes = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM)",
         "kernels": kernels,

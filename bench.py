@@ -646,6 +646,29 @@ def main():
     use_graph = not args.no_graph and not c_steps and (pg is None or dist.get_backend(pg) == "nccl" or
                                                        tr.peer is not None)
     step_fn = lambda: tr.step_cycle(rows, B, n_batches)  # noqa: E731
+    branch = os.environ.get("CEO_BENCH_BRANCH")
+    if branch:
+        # diagnostic (review r05 item 1): the price of a parallel branch in the
+        # captured graph -- forked before each step, joined after it, on a
+        # second stream; "empty": one tiny kernel (the fork / join edges alone),
+        # "gather": the next batch's X rows of both towers gathered into a
+        # contiguous staging tile (the branch's real work)
+        side = torch.cuda.Stream()
+        tiny = torch.zeros(64, device=dev)
+        stage = [torch.empty(B, tr.data[k].shape[1], device=dev) for k in ("firm_numeric", "ceo_numeric")]
+        nxt = rows[B:2 * B]
+
+        def step_fn():
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                if branch == "gather":
+                    for k, st in zip(("firm_numeric", "ceo_numeric"), stage):
+                        torch.index_select(tr.data[k], 0, nxt, out=st)
+                else:
+                    tiny.add_(1.0)
+            tr.step_cycle(rows, B, n_batches)
+            cur.wait_stream(side)
     for _ in range(args.warmup):
         step_fn()
     torch.cuda.synchronize()

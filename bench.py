@@ -156,6 +156,15 @@ def pmc_bytes_per_step(names):
     return None if not vals or any(v is None for v in vals) else float(sum(vals))
 
 
+def _finite(v):
+    """JSON-safe copy of a timing record: inf (a form not measured) -> None."""
+    if isinstance(v, dict):
+        return {k: _finite(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_finite(x) for x in v]
+    return None if isinstance(v, float) and not math.isfinite(v) else v
+
+
 def usable_cores():
     """CPUs this process may actually run on: the cgroup CPU quota when one
     is set (the GPU box gives each GPU a 16-CPU share of a 256-CPU host),
@@ -823,7 +832,11 @@ def main():
                    "exchange_vs_collective_us": (getattr(getattr(tr, "peer", None), "timing_us", None)),
                    # (in-reduction exchange, reduce -> exchange + Adam): device us per step, MAX over
                    # ranks, measured on the first data-parallel step; the faster form is used
-                   "fused_vs_two_launch_us": getattr(tr, "fused_vs_two_launch_us", None)},
+                   "fused_vs_two_launch_us": _finite(getattr(tr, "fused_vs_two_launch_us", None)),
+                   # every exchange form the validation timed (MAX over ranks; inf: not
+                   # bitwise equal to the reference form on some rank) and the one chosen
+                   "exchange_form": getattr(tr, "exchange_form", None),
+                   "exchange_form_us": _finite(getattr(tr, "exchange_form_us", None))},
         "mean_loss": round(loss, 5),
         "deterministic_ms_per_step": round(det_ms, 4) if det_ms is not None else None,
     }

@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 
 import torch
 
-TT_ABI_VERSION = 5
+TT_ABI_VERSION = 6
 TT_MAX_CAT = 16
 TT_SLOTS_PER_TOWER = 10
 TT_NUM_OFFSETS = 2 * TT_MAX_CAT + 2 * TT_SLOTS_PER_TOWER + 1
@@ -73,8 +73,12 @@ TT_AR_MAX_RANKS = 16
 TT_AR_HANDLE_BYTES = 64
 
 
+TT_AR_PULL, TT_AR_PUSH = 0, 1  # tt_ar_peers.protocol
+
+
 class TTArPeers(ctypes.Structure):  # tt_ar_peers
-    _fields_ = [("region", ctypes.c_void_p * TT_AR_MAX_RANKS)]
+    _fields_ = [("region", ctypes.c_void_p * TT_AR_MAX_RANKS), ("protocol", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 _LIB: Optional[ctypes.CDLL] = None

@@ -156,6 +156,8 @@ def choose_exchange_form(reference, candidates, restore, group=None, device=None
         local.append(math.inf if t is None else float(t))
     times = _max_over_ranks(local, group, device)
     out_t = {n: round(t, 2) for (n, _, _), t in zip([reference] + list(candidates), times)}
+    if prefer == ref_name:
+        return ref_name, out_t
     best, best_t = ref_name, times[0]
     for (name, _, _), go, t in zip(candidates, eligible, times[1:]):
         if not go:
@@ -200,6 +202,7 @@ class PeerExchange:
         self.peers = N.TTArPeers()
         for q, r in enumerate(regions):
             self.peers.region[q] = r
+        self.peers.protocol = N.TT_AR_PULL
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.wait_us = 0  # wait bound per launch (0: the library's 2 s)
         self.epoch = 0  # host epochs of the setup checks (before reset)
@@ -354,6 +357,19 @@ class PeerExchange:
                                          tr.grad.data_ptr(), tr.exp_avg.data_ptr(), tr.exp_avg_sq.data_ptr(),
                                          ctypes.byref(self.peers), self.rank, self.world, self.co_ranks,
                                          self.err.data_ptr(), int(self.wait_us), N.stream_ptr(self.device))
+
+    @property
+    def protocol(self) -> int:
+        """N.TT_AR_PULL (publish in the own region, flag, remote reads) or
+        N.TT_AR_PUSH (value|epoch words stored into every peer's region,
+        local polls); must be the same on every rank."""
+        return int(self.peers.protocol)
+
+    @protocol.setter
+    def protocol(self, p: int):
+        if p not in (N.TT_AR_PULL, N.TT_AR_PUSH):
+            raise ValueError(f"unknown exchange protocol {p}")
+        self.peers.protocol = int(p)
 
     def failed(self) -> bool:
         """True once any exchange on this rank timed out (reads err: syncs)."""

@@ -77,6 +77,7 @@ class FusedTrainer:
         # _validate_fused_exchange on the first data-parallel step
         self.fused_vs_two_launch_us = None
         self.exchange_form_us = None  # {form: us}, all forms timed by the validation
+        self.exchange_form = None     # the form it chose (engine._validate_fused_exchange)
         # TT_FLAG_DEFER_LATE: each single-GPU step leaves the late half of its
         # reduction (W4, BN1 affine, W8, logit_scale, the loss) to the next
         # step's first kernel; flush() finishes it (run automatically before
@@ -218,6 +219,7 @@ class FusedTrainer:
                 self.fused_exchange = True
                 return
             self.fused_exchange = False
+            self.peer.protocol = N.TT_AR_PULL  # (the validated two-launch form)
         self._launch(batch, n_rows, False)
         self.allreduce_and_adam()
 
@@ -261,19 +263,28 @@ class FusedTrainer:
             self._launch(batch, n_rows, False)
             self.allreduce_and_adam()
 
-        def run(fn):
+        def run(fn, proto):
             def go():
+                self.peer.protocol = proto
                 fn()
                 return result()
             return go
 
-        def timed(fn):
+        def timed(fn, proto):
             def go():
+                self.peer.protocol = proto
                 t = self._time_steps(fn)
                 if self.peer.failed():
                     raise RuntimeError("an exchange timed out while timing")
                 return t
             return go
+        # (name, step, protocol): the reference -- reduce, then the standalone
+        # pull exchange + Adam, itself checked against the collective -- and
+        # the candidates: the exchange inside the reduction (pull / push) and
+        # the standalone push exchange
+        pull, push = N.TT_AR_PULL, N.TT_AR_PUSH
+        forms = {"two_launch": (two_launch, pull), "fused": (fused_step, pull),
+                 "fused_push": (fused_step, push), "two_launch_push": (two_launch, push)}
 
         prev_det = self.deterministic
 
@@ -283,16 +294,19 @@ class FusedTrainer:
         self.deterministic = True  # the bitwise check in deterministic mode
         N.set_deterministic(self.desc, True)
         import os
+        entry = lambda k: (k, run(*forms[k]), timed(*forms[k]))  # noqa: E731
         try:
             use, times = choose_exchange_form(
-                ("two_launch", run(two_launch), timed(two_launch)),
-                [("fused", run(fused_step), timed(fused_step))], restore, self.pg, self.device,
-                prefer="fused" if os.environ.get("CEO_TT_FUSED_EX") == "1" else None, before_timing=steps_mode)
+                entry("two_launch"), [entry(k) for k in forms if k != "two_launch"], restore, self.pg, self.device,
+                prefer=os.environ.get("CEO_TT_EXCHANGE_FORM") or
+                ("fused" if os.environ.get("CEO_TT_FUSED_EX") == "1" else None), before_timing=steps_mode)
         finally:
             steps_mode()
         self.exchange_form_us = times
+        self.exchange_form = use
         self.fused_vs_two_launch_us = (times["fused"], times["two_launch"])
-        return use == "fused"
+        self.peer.protocol = forms[use][1]
+        return use in ("fused", "fused_push")
 
     def _time_steps(self, fn, k: int = 8) -> float:
         """Device time per step (us) of k back-to-back calls of ``fn``: the

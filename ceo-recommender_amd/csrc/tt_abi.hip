@@ -740,13 +740,18 @@ static void launch_reduce(const RedArgs& r, hipStream_t s, Evs ev = {}, bool ex 
 
 // ---- peer-memory exchange region (tt_ar_*): [flags of the standalone
 // exchange: TT_AR_MAX_RANKS x AR_BLOCKS][flags of the fused step:
-// TT_AR_MAX_RANKS x ar_red_blocks(n)][slot 0][slot 1] ----
+// TT_AR_MAX_RANKS x ar_red_blocks(n)][slot 0][slot 1][push words:
+// 2 parities x TT_AR_MAX_RANKS sources x ar_slot_floats(n), 8 B each] ----
 static constexpr int AR_BLOCKS = 32;
 static int64_t ar_slot_floats(int64_t n) { return (n + 63) / 64 * 64; }
+static int64_t ar_ll_bytes(int64_t n) { return 2 * (int64_t)TT_AR_MAX_RANKS * ar_slot_floats(n) * 8; }
 // k_reduce_adam blocks of any model with n parameters: every segment's
 // element range is at most 2 len + 64 long and starts on a block
 static int64_t ar_red_blocks(int64_t n) { return (2 * n) / RED_E + 2 * MAX_SEG + 1; }
 static int64_t ar_flag_bytes(int64_t n) { return (int64_t)TT_AR_MAX_RANKS * (AR_BLOCKS + ar_red_blocks(n)) * 8; }
+static uint64_t* ar_ll_base(void* region, int64_t n) {
+  return (uint64_t*)((char*)region + ar_flag_bytes(n) + 2 * ar_slot_floats(n) * (int64_t)sizeof(float));
+}
 
 // Deterministic mode: fold the per-block partial slots the kernel of stage
 // `pt` just stored into replica 0 of each accumulator (k_det_fold), or
@@ -1192,8 +1197,10 @@ int32_t tt_train_step_dp(const tt_model_desc* d, float* params, float* buffers, 
                          float* grad, float* exp_avg, float* exp_avg_sq, const tt_ar_peers* peers, int32_t rank,
                          int32_t world, int32_t co_ranks, int32_t* err, int64_t wait_us, tt_stream_t stream) {
   if (!peers || world < 1 || world > TT_AR_MAX_RANKS || rank < 0 || rank >= world || !err || co_ranks < 1 ||
-      !hp || !exp_avg || !exp_avg_sq || !desc_ok(d))
+      !hp || !exp_avg || !exp_avg_sq || !desc_ok(d) ||
+      (peers->protocol != TT_AR_PULL && peers->protocol != TT_AR_PUSH))
     return TT_ERR_ARG;
+  if (peers->protocol == TT_AR_PUSH && world > TT_AR_PUSH_MAX_RANKS) return TT_ERR_UNSUPPORTED;
   const int64_t n = make_layout(d).n;
   RedExchange x;
   std::memset(&x, 0, sizeof(x));
@@ -1202,7 +1209,9 @@ int32_t tt_train_step_dp(const tt_model_desc* d, float* params, float* buffers, 
     char* base = (char*)peers->region[q];
     x.flags[q] = (uint64_t*)(base + (int64_t)TT_AR_MAX_RANKS * AR_BLOCKS * 8);
     x.slot[q] = (float*)(base + ar_flag_bytes(n));
+    x.ll[q] = ar_ll_base(peers->region[q], n);
   }
+  x.protocol = peers->protocol;
   x.slot_stride = ar_slot_floats(n);
   x.rank = rank;
   x.world = world;
@@ -1737,7 +1746,7 @@ int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n
 // ar_flag_bytes above) ----
 int64_t tt_ar_region_bytes(int64_t n) {
   if (n < 1) return TT_ERR_ARG;
-  return ar_flag_bytes(n) + 2 * ar_slot_floats(n) * (int64_t)sizeof(float);
+  return ar_flag_bytes(n) + 2 * ar_slot_floats(n) * (int64_t)sizeof(float) + ar_ll_bytes(n);
 }
 
 int32_t tt_ar_alloc(int64_t bytes, void** region, void* ipc_handle) {
@@ -1783,7 +1792,8 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
                              float* grad_out, float* params, float* exp_avg, float* exp_avg_sq,
                              const tt_adam_hp* hp, tt_state* state, int64_t step_host, int32_t* err,
                              int64_t wait_us, tt_stream_t stream) {
-  if (!peers || world < 1 || world > TT_AR_MAX_RANKS || rank < 0 || rank >= world || n < 1 || !grad || !err)
+  if (!peers || world < 1 || world > TT_AR_MAX_RANKS || rank < 0 || rank >= world || n < 1 || !grad || !err ||
+      (peers->protocol != TT_AR_PULL && peers->protocol != TT_AR_PUSH))
     return TT_ERR_ARG;
   if (params && (!exp_avg || !exp_avg_sq || !hp)) return TT_ERR_ARG;
   if (!state && step_host < 1) return TT_ERR_ARG;
@@ -1794,6 +1804,7 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
     char* base = (char*)peers->region[q];
     a.flags[q] = (uint64_t*)base;
     a.slot[q] = (float*)(base + ar_flag_bytes(n));
+    a.ll[q] = ar_ll_base(peers->region[q], n);
   }
   a.slot_stride = ar_slot_floats(n);
   a.rank = rank;
@@ -1816,8 +1827,13 @@ int32_t tt_ar_allreduce_adam(const tt_ar_peers* peers, int32_t rank, int32_t wor
   a.err = err;
   // s_memrealtime runs at 100 MHz; default bound 2 s of polling, then give up (err)
   a.wait_ticks = (uint64_t)(wait_us > 0 ? wait_us : 2000000) * 100ull;
+  if (peers->protocol == TT_AR_PUSH && world > TT_AR_PUSH_MAX_RANKS) return TT_ERR_UNSUPPORTED;
   Range rg("tt_ar_exchange");
-  hipLaunchKernelGGL(k_ar_adam, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
+  if (peers->protocol == TT_AR_PUSH) {
+    hipLaunchKernelGGL(k_ar_adam_push, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL(k_ar_adam, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
+  }
   return launch_check();
 }
 

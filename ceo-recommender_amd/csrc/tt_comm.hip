@@ -36,6 +36,7 @@ constexpr int AR_THREADS = 256;
 struct ArArgs {
   float* slot[TT_AR_MAX_RANKS];          // slot 0 of each rank's region (slot 1 at + slot_stride)
   uint64_t* flags[TT_AR_MAX_RANKS];      // each rank's flag array [TT_AR_MAX_RANKS][blocks]
+  uint64_t* ll[TT_AR_MAX_RANKS];         // each rank's push words [2][TT_AR_MAX_RANKS][slot_stride] (TT_AR_PUSH)
   int64_t slot_stride;                   // floats between slot 0 and slot 1
   int rank, world, blocks;
   int64_t n;                             // gradient floats
@@ -156,6 +157,105 @@ __global__ __launch_bounds__(AR_THREADS) void k_ar_adam(ArArgs a) {
   else
     ar_mean_adam<TT_AR_MAX_RANKS>(a, lo, hi, par, c);
   if (a.p && a.state && b == 0 && threadIdx.x == 0) a.state->step_done = t;
+}
+
+// TT_AR_PUSH form of k_ar_adam (tt_common.h, ll_publish / ll_gather_sums),
+// the same AR_BLOCKS grid as the pull form (every block of a rank must be
+// resident while it waits for its peers: a grid sized by n could exceed what
+// the GPU holds at once and wait on itself).  Block b owns [lo, hi): every
+// lane stores its elements' words into every peer's region, then polls its
+// own region until all peers' words carry this step's epoch, and only then --
+// after a barrier that makes the outcome block-uniform -- applies the mean
+// and Adam: a block that timed out leaves its whole slice untouched, as the
+// pull form does.  A slice of one round (<= AR_EPT x AR_THREADS elements,
+// cfg 3) keeps the sums of the poll; a longer one polls every round first and
+// re-reads the (then settled) words for the sums.  No flags, no remote reads.
+template <int W>
+__device__ __forceinline__ void ar_push_block(const ArArgs& a, int64_t lo, int64_t hi, int64_t t, int* ok_s) {
+  const int64_t par = t & 1;
+  const uint32_t ep = (uint32_t)t;
+  constexpr int64_t RND = (int64_t)AR_EPT * AR_THREADS;
+  auto lanes = [&](int64_t e0, int64_t (&ec)[AR_EPT], bool (&live)[AR_EPT], float (&own)[AR_EPT]) {
+#pragma unroll
+    for (int j = 0; j < AR_EPT; ++j) {  // clamped: no branch around a load
+      const int64_t e = e0 + threadIdx.x + (int64_t)j * AR_THREADS;
+      live[j] = e < hi;
+      ec[j] = min(e, hi - 1);
+      own[j] = a.grad[ec[j]];
+    }
+  };
+  int64_t ec[AR_EPT];
+  bool live[AR_EPT];
+  float own[AR_EPT], s[AR_EPT];
+  for (int64_t e0 = lo; e0 < hi; e0 += RND) {  // publish the whole slice
+    lanes(e0, ec, live, own);
+#pragma unroll
+    for (int j = 0; j < AR_EPT; ++j)
+      if (live[j]) ll_publish(a.ll, a.world, a.rank, a.slot_stride, par, ec[j], own[j], ep);
+  }
+  AdamCoef c{};
+  if (a.p) c = adam_coef(a.lr, a.b1, a.b2, a.eps, t);
+  const bool one = hi - lo <= RND;  // (block-uniform)
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool fine = true;
+  for (int64_t e0 = lo; e0 < hi && fine; e0 += RND) {  // wait for every peer word of the slice
+    lanes(e0, ec, live, own);
+    fine = ll_gather_sums<W, AR_EPT>(a.ll[a.rank], a.world, a.rank, a.slot_stride, par, ec, live, own, ep, t0,
+                                     a.wait_ticks, s);
+  }
+  if (!fine) *ok_s = 0;
+  __syncthreads();
+  if (*ok_s == 0) {
+    if (threadIdx.x == 0) atomicAdd(a.err, 1);
+    return;
+  }
+  const float inv_w = 1.0f / (float)a.world;
+  for (int64_t e0 = lo; e0 < hi; e0 += RND) {
+    if (!one) {  // the words are settled: the sums of this round
+      lanes(e0, ec, live, own);
+      (void)ll_gather_sums<W, AR_EPT>(a.ll[a.rank], a.world, a.rank, a.slot_stride, par, ec, live, own, ep, t0,
+                                      ~0ull, s);
+    }
+    float p[AR_EPT], m[AR_EPT], v[AR_EPT];
+    if (a.p) {
+#pragma unroll
+      for (int j = 0; j < AR_EPT; ++j) {
+        p[j] = a.p[ec[j]];
+        m[j] = a.m[ec[j]];
+        v[j] = a.v[ec[j]];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < AR_EPT; ++j) {
+      if (!live[j]) continue;
+      const float g = s[j] * inv_w;
+      if (a.grad_out) a.grad_out[ec[j]] = g;
+      if (a.p) {
+        adam_elem(p[j], m[j], v[j], g, c);
+        a.p[ec[j]] = p[j];
+        a.m[ec[j]] = m[j];
+        a.v[ec[j]] = v[j];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(AR_THREADS) void k_ar_adam_push(ArArgs a) {
+  __shared__ int ok_s;
+  if (threadIdx.x == 0) ok_s = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  __syncthreads();
+  if (ok_s == 0) return;
+  const int64_t t = a.state ? load_step(a.state, reinterpret_cast<const int64_t*>(a.grad)) : a.step_host;
+  const int64_t per = (a.n + a.blocks - 1) / a.blocks;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(a.n, lo + per);
+  if (lo >= hi) return;  // (block-uniform)
+  if (a.world <= 2)
+    ar_push_block<2>(a, lo, hi, t, &ok_s);
+  else if (a.world <= 4)
+    ar_push_block<4>(a, lo, hi, t, &ok_s);
+  else
+    ar_push_block<8>(a, lo, hi, t, &ok_s);  // (the host allows the push protocol up to TT_AR_PUSH_MAX_RANKS = 8)
+  if (ok_s && a.p && a.state && blockIdx.x == 0 && threadIdx.x == 0) a.state->step_done = t;
 }
 
 }  // namespace tt

@@ -774,11 +774,84 @@ struct Seg {
 struct RedExchange {
   float* slot[TT_AR_MAX_RANKS];      // slot 0 of each rank's region (slot 1 at + slot_stride)
   uint64_t* flags[TT_AR_MAX_RANKS];  // each rank's fused-step flag array
+  uint64_t* ll[TT_AR_MAX_RANKS];     // each rank's push words [2 parities][TT_AR_MAX_RANKS sources][slot_stride]
   int64_t slot_stride;
   int32_t rank, world, blocks;
+  int32_t protocol;                  // TT_AR_PULL / TT_AR_PUSH (tt_ar_peers.protocol)
   int32_t* err;                      // set when a wait times out (sticky)
   uint64_t wait_ticks;               // wait bound in s_memrealtime ticks (100 MHz)
 };
+
+// Push protocol (TT_AR_PUSH): each exchanged element travels as ONE 8-byte
+// word -- the float's bits in the low half, the epoch (the step, mod 2^32)
+// in the high half -- stored by its owner straight into every peer's region
+// (row [t & 1][source rank]); a reader polls its OWN region until every
+// peer's word carries this epoch.  An aligned 8-byte store is single-copy
+// atomic, so a word with the right epoch holds the right value: no separate
+// flag, no release fence and no wait for the remote stores' completion
+// before signalling (the pull protocol's publish -> flag -> remote read is
+// three one-way trips; this is one).  Twice the bytes per element on the
+// links.  Row reuse: rank r rewrites row [t & 1][r] of peer q at step t + 2,
+// after its step-(t+1) reads saw q's step-(t+1) words, which q stored in a
+// launch that began after its step-t reads ended (stream order).
+__device__ __forceinline__ uint64_t ll_word(float v, uint32_t ep) {
+  return ((uint64_t)ep << 32) | (uint64_t)__float_as_uint(v);
+}
+// owner lane: this rank's value of element e into every peer's row
+__device__ __forceinline__ void ll_publish(uint64_t* const* ll, int world, int rank, int64_t row_stride,
+                                           int64_t par, int64_t e, float v, uint32_t ep) {
+  const uint64_t w = ll_word(v, ep);
+  const int64_t off = (par * TT_AR_MAX_RANKS + rank) * row_stride + e;
+  for (int q = 0; q < world; ++q)
+    if (q != rank) __hip_atomic_store(ll[q] + off, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// wait (bounded) until every peer's word of this lane's EPT elements e[j]
+// (live[j]) in this rank's own region carries epoch ep, then the rank-order
+// sums with this rank's own terms from the registers -- the same adds as
+// rank_order_sums, so both protocols give every rank bitwise the same mean.
+// All EPT x W polls are in flight at once; only the words still stale are
+// re-read.  False on timeout (out[] then undefined).
+template <int W, int EPT>
+__device__ __forceinline__ bool ll_gather_sums(const uint64_t* own_ll, int world, int rank, int64_t row_stride,
+                                               int64_t par, const int64_t* e, const bool* live, const float* own,
+                                               uint32_t ep, uint64_t t0, uint64_t bound, float* out) {
+  uint64_t x[EPT][W];
+  auto src = [&](int j, int r) {
+    const int q = (r < world && r != rank) ? r : rank;  // inactive: this rank's own (unused) row, a valid address
+    return own_ll + (par * TT_AR_MAX_RANKS + q) * row_stride + e[j];
+  };
+  auto want = [&](int j, int r) { return live[j] && r < world && r != rank; };
+#pragma unroll
+  for (int j = 0; j < EPT; ++j)
+#pragma unroll
+    for (int r = 0; r < W; ++r) x[j][r] = __hip_atomic_load(src(j, r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    bool done = true;
+#pragma unroll
+    for (int j = 0; j < EPT; ++j)
+#pragma unroll
+      for (int r = 0; r < W; ++r)
+        if (want(j, r) && (uint32_t)(x[j][r] >> 32) != ep) done = false;
+    if (done) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > bound) return false;
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int j = 0; j < EPT; ++j)
+#pragma unroll
+      for (int r = 0; r < W; ++r)
+        if (want(j, r) && (uint32_t)(x[j][r] >> 32) != ep)
+          x[j][r] = __hip_atomic_load(src(j, r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < W; ++r)
+      if (r < world) s += r == rank ? own[j] : __uint_as_float((uint32_t)x[j][r]);
+    out[j] = s;
+  }
+  return true;
+}
 
 // Rank-order sum of one exchanged element: the peers' slot values, this
 // rank's own term from the register (the bits its slot holds).  All W loads

@@ -6,7 +6,9 @@
 namespace tt {
 
 // Data-parallel exchange of the reduced gradient (EX instance; all threads of
-// the block call it, owner lanes carry an element).  The one-shot protocol of
+// the block call it, owner lanes carry an element).  TT_AR_PUSH: the
+// flag-in-data words of tt_common.h (ll_publish / ll_gather_sums), one
+// barrier.  TT_AR_PULL: the one-shot protocol of
 // tt_comm.hip (k_ar_adam) per reduction block: publish this block's sums into
 // this rank's slot[t & 1], signal flag[rank][block] = t on every peer, wait
 // (bounded) for every peer's flag, then the mean in rank order -- this rank's
@@ -21,6 +23,34 @@ __device__ __forceinline__ bool reduce_exchange(const RedExchange& X, int64_t t,
                                                 int* ok_s) {
   if (*ok_s == 0) return false;
   if (X.world == 1) return true;
+  if (X.protocol == TT_AR_PUSH) {  // this element's word into every peer, then poll the own region
+    const int64_t par = t & 1;
+    const uint32_t ep = (uint32_t)t;
+    bool fine = true;
+    if (owner) {
+      ll_publish(X.ll, X.world, X.rank, X.slot_stride, par, e, g, ep);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const bool live = true;
+      float s = 0.f;
+      if (X.world <= 2)
+        fine = ll_gather_sums<2, 1>(X.ll[X.rank], X.world, X.rank, X.slot_stride, par, &e, &live, &g, ep, t0,
+                                    X.wait_ticks, &s);
+      else if (X.world <= 4)
+        fine = ll_gather_sums<4, 1>(X.ll[X.rank], X.world, X.rank, X.slot_stride, par, &e, &live, &g, ep, t0,
+                                    X.wait_ticks, &s);
+      else  // (the host allows the push protocol up to TT_AR_PUSH_MAX_RANKS = 8)
+        fine = ll_gather_sums<8, 1>(X.ll[X.rank], X.world, X.rank, X.slot_stride, par, &e, &live, &g, ep, t0,
+                                    X.wait_ticks, &s);
+      if (fine) g = s * (1.0f / (float)X.world);
+    }
+    if (!fine) *ok_s = 0;  // (every writer stores 0)
+    __syncthreads();
+    if (*ok_s == 0) {  // block-uniform: this block's parameters stay untouched
+      if (threadIdx.x == 0) atomicAdd(X.err, 1);
+      return false;
+    }
+    return true;
+  }
   const uint64_t epoch = (uint64_t)t;
   const int b = blockIdx.x, q = threadIdx.x;
   const int64_t par = (t & 1) ? X.slot_stride : 0;

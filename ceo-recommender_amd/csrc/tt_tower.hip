@@ -609,7 +609,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   // for them alone), then this lane's A-operand slices of Z0: row 16w + r,
   // columns 8g.. and 32 + 8g..
   RepSum1<NTH, 2 * H0> rs;
+#ifdef TT_DIAG_REP
+  rs.issue(T.Z0 + (int64_t)(a.B / 2) * H0, 2 * H0);  // diagnostic (wrong values): plain-stored lines instead of the atomically built replicas
+#else
   rs.issue(T.st0, 2 * H0);
+#endif
   float bias[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias[j] = T.b4[16 * j + r];
@@ -636,7 +640,9 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   const float4 zb0 = *reinterpret_cast<const float4*>(zr + 32), zb1 = *reinterpret_cast<const float4*>(zr + 36);
   const bool drop = a.train && a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
+  TT_STAMP(1, 1);
   if (a.train) rs.finish(rsc, rst);
+  TT_STAMP(1, 2);
   if (threadIdx.x < H0) {
     const int c = threadIdx.x;
     float mean, inv;
@@ -651,13 +657,14 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     if (a.train)
       a0r[c] = bn_relu_drop(z0r, mean, alpha, bn_be, drop, dropout_row_key(key, 0), c, a.drop_thr, a.drop_scale);
   }
+  TT_STAMP(1, 3);
 #pragma unroll
   for (int k = 0; k < W4T; ++k) {
     const int we = (int)threadIdx.x + k * NTH;
     put_planes4(Wh + (we >> 4) * LDK + 4 * (we & 15), PL, w4v[k]);
   }
   __syncthreads();
-  TT_STAMP(1, 1);
+  TT_STAMP(1, 4);
 
   // ---- A0 of this lane's 16 elements (columns c = 8g + e and c + 32), split
   // into the two K steps' A operands
@@ -693,7 +700,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     split8x3(x0, xa[0]);
     split8x3(x1, xa[1]);
   }
-  TT_STAMP(1, 2);
+  TT_STAMP(1, 5);
 
   // ---- Z4 = A0 W4^T (bf16x3, two K steps per 16-column tile); waves 0 and 1
   // also compute tile w of the shift row with the same MFMA sequence in every
@@ -740,7 +747,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     }
     __syncthreads();  // shl
   }
-  TT_STAMP(1, 3);
+  TT_STAMP(1, 6);
 
   float s1[2], s2[2];
 #pragma unroll
@@ -769,7 +776,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
     if (threadIdx.x < 2 * H1)
       xblock_add(a.det, T.st1, 2 * H1, T.dslot, 2 * H1, threadIdx.x, wave_rows_sum<NW>(red, 2 * H1, threadIdx.x));
   }
-  TT_STAMP(1, 4);
+  TT_STAMP(1, 7);
 }
 
 // ---------------------------------------------------------------------------

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TT_ABI_VERSION 5
+#define TT_ABI_VERSION 6
 #define TT_MAX_CAT 16      /* categorical columns per tower */
 
 /* status codes */
@@ -420,8 +420,21 @@ int32_t tt_triplet_backward(const float* f, const float* c, int64_t m, int64_t n
  * re-creating the exchange (tt_ar_reset on every rank).                   */
 #define TT_AR_MAX_RANKS 16
 #define TT_AR_HANDLE_BYTES 64
+/* exchange protocols (tt_ar_peers.protocol; zero-initialised = pull):
+ * TT_AR_PULL: each rank stores its slice into its OWN region, raises a flag
+ *   in every peer's region, waits for the peers' flags and reads their slices
+ *   remotely.
+ * TT_AR_PUSH: each rank stores every element as one 8-byte word (value |
+ *   epoch) straight into every PEER's region and polls its own region until
+ *   all peers' words carry this step's epoch: no flags, no remote reads.
+ * Both sum in rank order: bitwise the same mean.  (ABI 6)                   */
+#define TT_AR_PULL 0
+#define TT_AR_PUSH 1
+#define TT_AR_PUSH_MAX_RANKS 8  /* push: world <= 8 (one node), else TT_ERR_UNSUPPORTED */
 typedef struct tt_ar_peers {
   void* region[TT_AR_MAX_RANKS];   /* every rank's region, mapped in this process */
+  int32_t protocol;                /* TT_AR_PULL or TT_AR_PUSH; the same on every rank */
+  int32_t reserved;
 } tt_ar_peers;
 int64_t tt_ar_region_bytes(int64_t n);
 int32_t tt_ar_alloc(int64_t bytes, void** region, void* ipc_handle);

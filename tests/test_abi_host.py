@@ -290,3 +290,12 @@ def test_embedding_mining_exchange_host_argument_errors():
     assert run(0, 2, 100, None) == N.TT_ERR_ARG
     assert run(0, 3, 100, p) == N.TT_ERR_ARG          # region of rank 2 missing
     assert run(0, 2, 100, p, step=0) == N.TT_ERR_ARG  # no device state: host epochs start at 1
+    # protocol field (ABI 6): unknown values refused; push above 8 ranks unsupported
+    peers.protocol = 7
+    assert run(0, 2, 100, p) == N.TT_ERR_ARG
+    peers.protocol = N.TT_AR_PUSH
+    for q in range(9):
+        peers.region[q] = p
+    assert run(0, 9, 100, p) == N.TT_ERR_UNSUPPORTED
+    peers.protocol = N.TT_AR_PULL
+    assert (header_define("TT_AR_PULL"), header_define("TT_AR_PUSH")) == (N.TT_AR_PULL, N.TT_AR_PUSH)

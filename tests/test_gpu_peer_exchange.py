@@ -339,11 +339,12 @@ def test_exchange_inside_reduction_matches_two_launch_form(world):
     print(f"world {world}: fused vs two-launch step us {res[0][3]}")
 
 
-def test_exchange_inside_reduction_timeout_leaves_parameters():
+@pytest.mark.parametrize("protocol", ["pull", "push"])
+def test_exchange_inside_reduction_timeout_leaves_parameters(protocol):
     """tt_train_step_dp with a peer that never runs: the reduction's waits
     time out, parameters / Adam moments stay at their values (never an
     update from the local gradient alone), later steps are device-side
-    no-ops for the exchange, and the host check raises."""
+    no-ops for the exchange, and the host check raises -- on both protocols."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import ctypes
@@ -366,6 +367,7 @@ def test_exchange_inside_reduction_timeout_leaves_parameters():
     ex = PeerExchange(L, regs, regs[0], 0, 2, n, dev)
     ex.regions = [regs[0], None]
     ex.wait_us = 20_000
+    ex.protocol = N.TT_AR_PUSH if protocol == "push" else N.TT_AR_PULL
     try:
         tr.peer, tr.dp, tr.world, tr.fused_exchange = ex, True, 2, True  # (no validation: the peer never runs)
         shard = {k: torch.from_numpy(v) for k, v in sub(g, "G2/shard0").items()}
@@ -455,6 +457,179 @@ def test_failed_exchange_leaves_no_stale_embedding_gradients():
             assert normwise(got, grads[name].numpy()) < 1e-5, name
             checked += 1
         assert checked == len(meta["firm_cat_counts"]) + len(meta["ceo_cat_counts"])
+    finally:
+        torch.cuda.synchronize()
+        L.tt_ar_free(ctypes.c_void_p(regs[1]))
+        ex.close()
+
+
+# ---- the push protocol (TT_AR_PUSH, round 6): value|epoch words stored into
+# every peer's region, local polls -- bitwise the pull protocol's mean ------
+
+def _push_vs_pull_rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching import _native as N
+        from ceo_firm_matching.distributed import PeerExchange
+        dev = torch.device("cuda:0")
+        res = {}
+        for n in (21313, 300_017):  # cfg 3's arena; a slice of > AR_EPT x 256 per 32 blocks
+            ex = PeerExchange.create(n, dist.group.WORLD, dev, mode="1")
+            assert ex is not None, "peer exchange could not be set up"
+            hp = N.adam_hp(4e-4)
+            for proto in (N.TT_AR_PULL, N.TT_AR_PUSH):
+                ex.reset(dist.group.WORLD)
+                ex.protocol = proto
+                p = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(7))
+                m = torch.zeros(n, device=dev)
+                v = torch.zeros(n, device=dev)
+                outs = []
+                for step in range(1, 5):  # both parities, epochs > 2
+                    x = torch.randn(n, generator=torch.Generator().manual_seed(100 * step + rank)).to(dev)
+                    out = torch.empty_like(x)
+                    ex.run(x, grad_out=out, params=p, exp_avg=m, exp_avg_sq=v, hp=hp, step_host=step)
+                    torch.cuda.synchronize()
+                    assert int(ex.err.item()) == 0, (proto, step)
+                    outs.append(out.cpu().numpy().copy())
+                res[(n, proto)] = (np.concatenate(outs), p.cpu().numpy().copy(), m.cpu().numpy().copy(),
+                                   v.cpu().numpy().copy())
+            ex.close()
+        same = all(all(np.array_equal(a, b) for a, b in zip(res[(n, N.TT_AR_PULL)], res[(n, N.TT_AR_PUSH)]))
+                   for n in (21313, 300_017))
+        digest = [res[k][0].tobytes() for k in sorted(res)]
+        allo = [None] * world
+        dist.all_gather_object(allo, digest)
+        q.put((rank, same, all(a == allo[0] for a in allo)))
+    except Exception as e:
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_push_exchange_bitwise_equals_pull(world):
+    """The standalone exchange + Adam on the push protocol: every grad_out,
+    parameter and Adam moment bitwise the pull protocol's, over four steps
+    (both parities), at n = cfg 3's arena and at 300k elements (a grid of more
+    than the pull form's 32 blocks), the same on every rank."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    for rank, same, ranks_equal in _spawn(_push_vs_pull_rank, world):
+        assert same is True, (rank, same)
+        assert ranks_equal is True, rank
+
+
+def _forms_rank(rank, world, port, q, steps):
+    """Every exchange form of the data-parallel step forced in turn
+    (CEO_TT_EXCHANGE_FORM: chosen when the validation finds it bitwise equal
+    to the reference form), K deterministic steps each: bitwise the same
+    parameters, moments and buffers whichever form runs."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CEO_TT_PEER_AR="1", CEO_TT_FUSED_EX="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ceo_firm_matching.engine import FusedTrainer
+        dev = torch.device("cuda:0")
+        g = load_golden("ddp")
+        shard = {k: torch.from_numpy(v) for k, v in sub(g, f"G2/shard{rank % 2}").items()}
+        B = shard["target"].shape[0]
+        outs, chosen, times = {}, {}, None
+        for form in ("fused", "fused_push", "two_launch", "two_launch_push"):
+            os.environ["CEO_TT_EXCHANGE_FORM"] = form
+            m = _cfg2_model(dev, g)
+            tr = FusedTrainer(m, lr=4e-4, max_batch=B, seed=5, process_group=dist.group.WORLD, deterministic=True)
+            tr.set_data(shard)
+            for _ in range(steps):
+                tr.step(None, 0, B)
+            tr.pop_loss_sum()
+            chosen[form] = tr.exchange_form
+            times = tr.exchange_form_us
+            outs[form] = np.concatenate([tr.arena.params.cpu().numpy(), tr.exp_avg.cpu().numpy(),
+                                         tr.exp_avg_sq.cpu().numpy(), tr.arena.buffers.cpu().numpy()])
+            tr.peer.close()
+        os.environ.pop("CEO_TT_EXCHANGE_FORM")
+        same = all(np.array_equal(outs["fused"], o) for o in outs.values())
+        q.put((rank, same, chosen, times))
+    except Exception as e:
+        q.put((rank, repr(e), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_every_exchange_form_gives_the_same_step(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    res = _spawn(_forms_rank, world, 3)
+    for rank, same, chosen, times in res:
+        assert same is True, (rank, same)
+        assert chosen == {f: f for f in chosen}, (rank, chosen)  # each forced form passed the bitwise check
+        assert set(times) == {"two_launch", "fused", "fused_push", "two_launch_push"}, times
+    print(f"world {world}: exchange form us {res[0][3]}")
+
+
+def test_push_exchange_timeout_leaves_parameters_and_raises():
+    """The standalone push exchange with a peer that never runs: every block
+    times out and leaves its slice of params / exp_avg / exp_avg_sq /
+    grad_out untouched, the words it stored are in the peer's region (epoch
+    1, this rank's row), later launches are device-side no-ops, the host
+    check raises."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ctypes
+    from ceo_firm_matching import _native as N
+    from ceo_firm_matching.distributed import PeerExchange
+    L = N.lib()
+    dev = torch.device("cuda:0")
+    n = 5000
+    nbytes = int(L.tt_ar_region_bytes(n))
+    regs = []
+    for _ in range(2):
+        r = ctypes.c_void_p()
+        h = (ctypes.c_uint8 * N.TT_AR_HANDLE_BYTES)()
+        N.check(L.tt_ar_alloc(nbytes, ctypes.byref(r), h), "tt_ar_alloc")
+        regs.append(r.value)
+    ex = PeerExchange(L, regs, regs[0], 0, 2, n, dev)
+    ex.regions = [regs[0], None]
+    ex.wait_us = 20_000
+    ex.protocol = N.TT_AR_PUSH
+    try:
+        g = torch.Generator(device=dev).manual_seed(3)
+        p = torch.randn(n, device=dev, generator=g)
+        m = torch.randn(n, device=dev, generator=g).abs()
+        v = torch.randn(n, device=dev, generator=g).abs()
+        x = torch.randn(n, device=dev, generator=g)
+        out = torch.full((n,), 7.0, device=dev)
+        p0, m0, v0 = p.clone(), m.clone(), v.clone()
+        hp = N.adam_hp(4e-4)
+        ex.run(x, grad_out=out, params=p, exp_avg=m, exp_avg_sq=v, hp=hp, step_host=1)
+        torch.cuda.synchronize()
+        assert ex.failed()
+        assert torch.equal(p, p0) and torch.equal(m, m0) and torch.equal(v, v0)
+        assert bool((out == 7.0).all())
+        # the peer's region holds this rank's words: row [parity 1][source 0], epoch 1 | x
+        slot = (n + 63) // 64 * 64
+        ll_off = nbytes - 2 * N.TT_AR_MAX_RANKS * slot * 8
+        words = torch.empty(n, dtype=torch.int64, device=dev)
+        hip = ctypes.CDLL("libamdhip64.so")
+        row = ll_off + (1 * N.TT_AR_MAX_RANKS + 0) * slot * 8
+        assert hip.hipMemcpy(ctypes.c_void_p(words.data_ptr()), ctypes.c_void_p(regs[1] + row),
+                             ctypes.c_size_t(n * 8), 3) == 0
+        torch.cuda.synchronize()
+        w = words.cpu().numpy().view(np.uint64)
+        assert bool(((w >> np.uint64(32)) == 1).all())
+        assert np.array_equal((w & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32), x.cpu().numpy())
+        err_before = int(ex.err.item())
+        ex.run(x, grad_out=out, params=p, exp_avg=m, exp_avg_sq=v, hp=hp, step_host=2)  # sticky
+        torch.cuda.synchronize()
+        assert int(ex.err.item()) == err_before
+        assert torch.equal(p, p0) and bool((out == 7.0).all())
+        with pytest.raises(RuntimeError, match="did not publish"):
+            ex.check()
     finally:
         torch.cuda.synchronize()
         L.tt_ar_free(ctypes.c_void_p(regs[1]))

@@ -71,6 +71,22 @@ template <int BM_, int BN_, int WN_, int NP_ = 0> struct Cfg {
 #ifndef TT_NCE_WS
 #define TT_NCE_WS 0  // measured slower (r03: fwd 34.2 vs 29.6 ms, ranks 31.8 vs 25.5 ms)
 #endif
+// fp32 operand stages (round 6, measured, not the default): the similarity kernels stage
+// raw fp32 tiles in LDS -- 64 KB per 256 x 256 x 32 stage instead of 96 KB of
+// bf16 planes -- so TWO stages fit: chunk c + 1 is copied in (global -> VGPR
+// -> ds_write_b128, no arithmetic) while chunk c's MFMAs run, one barrier per
+// chunk, and each wave splits its own fragments into the three bf16 planes
+// right after reading them (3x the split work of splitting at staging, but
+// issued between the MFMAs, not in a phase of its own).  Same plane values,
+// same K order and six-product order: bitwise the same similarities.
+// Measured (tools/gpu_nce_check.sh, two interleaved rounds, N = 100k, D =
+// 256; contrastive GPU tests green): forward 28.2 -> 32.2 ms, ranks 23.9 ->
+// 27.8 ms -- each wave splits its 4 A and 8 B fragments itself, 3x the VALU
+// of the single split at staging (B tiles split by all 4 M-waves), and the A
+// fragments' split at the top of each chunk is not hidden.
+#ifndef TT_NCE_F32LDS
+#define TT_NCE_F32LDS 0  // measured slower (round 6: fwd 28.2 -> 32.2 ms, ranks 23.9 -> 27.8 ms at N = 100k, D = 256)
+#endif
 #if TT_NCE_WS
 using CfgSim = Cfg<128, 256, 128, 4>;
 #elif TT_NCE_SIM_DB
@@ -121,8 +137,9 @@ __device__ __forceinline__ int lds_off(int m, int k) {  // bf16 offset of (m, k)
 // one stage = A (BM rows) + B (BN rows), in bf16 elements
 template <class C, bool SWZ>
 constexpr int stage_elems() { return Lay<SWZ, C::BM>::OPND + Lay<SWZ, C::BN>::OPND; }
-constexpr size_t LDS_SIM =
-    sizeof(uint16_t) * ((TT_NCE_SIM_DB || TT_NCE_WS) ? 2 : 1) * stage_elems<CfgSim, true>();  // 96 / 144 KB
+constexpr size_t LDS_SIM = (TT_NCE_F32LDS && !TT_NCE_WS && !TT_NCE_SIM_DB)
+    ? sizeof(float) * 2 * (CfgSim::BM + CfgSim::BN) * BK                                       // 128 KB
+    : sizeof(uint16_t) * ((TT_NCE_SIM_DB || TT_NCE_WS) ? 2 : 1) * stage_elems<CfgSim, true>();  // 96 / 144 KB
 constexpr size_t LDS_GRAD = sizeof(uint16_t) * stage_elems<CfgGrad, false>();                        // 120 KB
 static_assert(LDS_SIM <= 160 * 1024 && LDS_GRAD <= 160 * 1024, "LDS per CU");
 
@@ -506,6 +523,91 @@ __device__ __forceinline__ void gemm_loop_db(const GemmArgs& g_, int64_t m0, int
   mma();
 }
 
+// fp32-stage main loop (TT_NCE_F32LDS, both operands SRC_MK).  Stage layout:
+// A rows [BM][32 floats] then B rows [BN][32 floats]; 16-B granule q of row m
+// sits at q ^ f32_swz(m) -- a table found by search against the gfx950
+// ds_read_b128 lane groups (MI355X_MICROARCH.md LDS table): the fragment
+// reads (lane (r, g): row 16t + r, granules 2g and 2g + 1) are conflict-free,
+// and so are the staging writes (4 lanes per row, one granule each).
+__device__ __forceinline__ int f32_swz(int m) {
+  // rows 0..15: 7 6 3 3 6 6 4 2 7 3 2 0 2 7 1 5 (3 bits each)
+  constexpr uint64_t T = 7ull | 6ull << 3 | 3ull << 6 | 3ull << 9 | 6ull << 12 | 6ull << 15 | 4ull << 18 |
+                         2ull << 21 | 7ull << 24 | 3ull << 27 | 2ull << 30 | 0ull << 33 | 2ull << 36 | 7ull << 39 |
+                         1ull << 42 | 5ull << 45;
+  return (int)((T >> (3 * (m & 15))) & 7);
+}
+__device__ __forceinline__ int f32_off(int m, int q) { return m * BK + ((q ^ f32_swz(m)) << 2); }
+
+// 8 consecutive k (k-octet g) of row m from an fp32 stage, split into planes
+__device__ __forceinline__ void frag32(const float* S, int m, int g, bf16x8 (&pl)[NPL]) {
+  const float4 u = *reinterpret_cast<const float4*>(S + f32_off(m, 2 * g));
+  const float4 v = *reinterpret_cast<const float4*>(S + f32_off(m, 2 * g + 1));
+  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  split8x3(x, pl);
+}
+
+template <class C>
+__device__ __forceinline__ void gemm_loop_f32(const GemmArgs& g_, int64_t m0, int64_t n0, float* smem,
+                                              f32x4 (&acc)[TM][C::TN]) {
+  constexpr int NT = C::NTH, TN = C::TN, BM_ = C::BM, BN = C::BN;
+  constexpr int STAGE = (BM_ + BN) * BK;  // floats
+  const int w = wave_id(), l = lane_id(), r = l & 15, g = l >> 4;
+  const int wm = w / C::NWN, wn = w % C::NWN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  const int nch = (int)((g_.A.kdim + BK - 1) / BK);
+  if (nch <= 0) return;
+  float4 va[BM_ * 8 / NT], vb[BN * 8 / NT];
+  auto fetch = [&](int c) {  // loads past K return zeros (buffer range)
+    load_opnd<SRC_MK, BM_, NT>(g_.A, m0, (int64_t)c * BK, va);
+    load_opnd<SRC_MK, BN, NT>(g_.B, n0, (int64_t)c * BK, vb);
+  };
+  auto put = [&](float* S) {  // item e: row e >> 2, granules 2 (e & 3) and + 1
+#pragma unroll
+    for (int t = 0; t < BM_ * 4 / NT; ++t) {
+      const int e = (int)threadIdx.x + t * NT, m = e >> 2, q = 2 * (e & 3);
+      *reinterpret_cast<float4*>(S + f32_off(m, q)) = va[2 * t];
+      *reinterpret_cast<float4*>(S + f32_off(m, q + 1)) = va[2 * t + 1];
+    }
+    float* SB = S + BM_ * BK;
+#pragma unroll
+    for (int t = 0; t < BN * 4 / NT; ++t) {
+      const int e = (int)threadIdx.x + t * NT, m = e >> 2, q = 2 * (e & 3);
+      *reinterpret_cast<float4*>(SB + f32_off(m, q)) = vb[2 * t];
+      *reinterpret_cast<float4*>(SB + f32_off(m, q + 1)) = vb[2 * t + 1];
+    }
+  };
+  fetch(0);
+  put(smem);
+  if (nch > 1) fetch(1);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const float* S = smem + (c & 1) * STAGE;
+    // chunk c + 1 into the other stage (its readers, chunk c - 1, passed the
+    // last barrier) and chunk c + 2's loads in flight, beside chunk c's MFMAs
+    if (c + 1 < nch) {
+      put(smem + ((c + 1) & 1) * STAGE);
+      if (c + 2 < nch) fetch(c + 2);
+    }
+    bf16x8 a[TM][NPL];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) frag32(S, wm * WM + 16 * i + r, g, a[i]);
+    bf16x8 b[2][NPL];
+    frag32(S + BM_ * BK, wn * C::WN + r, g, b[0]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j + 1 < TN) frag32(S + BM_ * BK, wn * C::WN + 16 * (j + 1) + r, g, b[(j + 1) & 1]);
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = mfma_bf16(a[i][PA[q]], b[j & 1][PB[q]], acc[i][j]);
+    }
+    __syncthreads();
+  }
+}
+
 // Warp-specialised main loop (TT_NCE_WS, both operands SRC_MK, swizzled LDS):
 // stage c & 1 holds chunk c.  Producer waves (w >= NW) stored chunk c + 1
 // into stage (c + 1) & 1 and issue chunk c + 2's loads while the MFMA waves
@@ -633,6 +735,8 @@ __global__ __launch_bounds__(CfgSim::NTH) void k_nce_sim(GemmArgs a) {
   if (wave_id() >= C::NW) return;  // producers: no epilogue
 #elif TT_NCE_SIM_DB
   gemm_loop_db<C>(a, m0, n0, smem, acc);
+#elif TT_NCE_F32LDS
+  gemm_loop_f32<C>(a, m0, n0, reinterpret_cast<float*>(smem), acc);
 #else
   gemm_loop<SRC_MK, SRC_MK, C, false, (bool)TT_NCE_PIPE>(a, m0, n0, 0, a.A.kdim, smem, acc);
 #endif

@@ -603,6 +603,10 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   float* rsc = smem + L::f_rsc;                      // [NTH] replica-sum scratch
   float* rst = smem + L::f_rst;                      // [2*64] BN0 moment sums S1|S2
   TT_STAMP(1, 0);
+#ifdef TT_DIAG_KARG  // diagnostic stamps build: slot 1 = when the kernel arguments have arrived
+  asm volatile("; karg %0 %1" ::"s"(a.tw[0].st0), "s"(a.state));
+  TT_STAMP(1, 1);
+#endif
 
   // ---- issue every load of the phase first (Z0 rows are padded: no clamp):
   // the BN0 moment replicas first (their sum and the coefficient chain wait
@@ -640,7 +644,9 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   const float4 zb0 = *reinterpret_cast<const float4*>(zr + 32), zb1 = *reinterpret_cast<const float4*>(zr + 36);
   const bool drop = a.train && a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
+#ifndef TT_DIAG_KARG
   TT_STAMP(1, 1);
+#endif
   if (a.train) rs.finish(rsc, rst);
   TT_STAMP(1, 2);
   if (threadIdx.x < H0) {

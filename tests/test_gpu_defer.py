@@ -205,6 +205,7 @@ def test_workspace_growth_flushes_the_pending_late_half():
     deferral record live there) must run first.  Deferred steps
     of 8192 rows on an 8192-row workspace, then 16384-row steps: the same
     training as plain steps, loss included."""
+    from ceo_firm_matching import _native as N
     _, _, data, make = _setup(p=0.0)
     sizes = [B // 2, B // 2, B, B]
     out = []
@@ -217,9 +218,20 @@ def test_workspace_growth_flushes_the_pending_late_half():
         assert tr.max_batch == B and tr.steps_done() == len(sizes)
         loss = tr.pop_loss_sum()
         sd = m.state_dict()
-        out.append(({k: v.detach().cpu().double().numpy().copy() for k, v in sd.items()}, loss))
-    (a, la), (b, lb) = out
+        mom = {}
+        for name, prm, off in m._named_slots(N.param_offsets(tr.desc)):
+            mom[name] = tuple(t[off:off + prm.numel()].cpu().double().numpy().copy() for t in (tr.exp_avg, tr.exp_avg_sq))
+        out.append(({k: v.detach().cpu().double().numpy().copy() for k, v in sd.items()}, loss, mom))
+    (a, la, ma), (b, lb, mb) = out
     assert abs(la - lb) <= 1e-5 * abs(la), (la, lb)
+    # Adam moments of every parameter but the pre-BN biases: normwise, at the
+    # gradients' reduction-order level (a lost late half would leave W4 / W8 /
+    # logit_scale's moments a whole step behind: O(1) relative)
+    for k in ma:
+        if excluded_param(k):
+            continue
+        for i, what in enumerate(("exp_avg", "exp_avg_sq")):
+            assert normwise(mb[k][i], ma[k][i]) < 1e-4, (k, what, normwise(mb[k][i], ma[k][i]))
     # parameters at the optimizer-scale bound (the late half sums its slabs in
     # another fixed order; the pre-BN biases, whose true gradient is 0, and
     # the running means that carry them are excluded as everywhere else): a

@@ -22,8 +22,15 @@ constexpr int MAX_KP = 256;  // padded tower input width supported by the fused 
 // accumulated into NREP replicas picked by blockIdx.x: 512 blocks adding into
 // the same 128 addresses serialise at the memory-side atomic unit (measured:
 // +4.5 us on k_l0_fwd); with replicas each address sees 1/NREP of the adds and
-// the consumers sum NREP values.
-constexpr int NREP = 16;
+// the consumers sum NREP values.  NREP = 8 (round 6; was 16): every block of
+// one XCD (blockIdx % 8) adds into that XCD's replica, and every consumer
+// block (all of k_l4_fwd's 512, the reduction's replica ranges) loads half
+// the bytes.  Two interleaved rounds at cfg 3 (profiles/r06_nrep_ab): step
+// 16: 49.6-49.7 us, 8: 49.2, 4: 50.5-50.6, 2: 56.1 (the adds serialise again).
+#ifndef TT_NREP
+#define TT_NREP 8
+#endif
+constexpr int NREP = TT_NREP;
 constexpr int BNG = 2 * H0 + 2 * H1;  // one replica of a tower's BN-affine grads: gg0|gbe0|gg1|gbe1
 // Folded BN0 backward (k_bwd_mid<R, true>, numeric-only towers with kp <= 64):
 // one replica of a tower's fold sums: gg0 | gbe0 | sum Zhat0 | sum (X - shift)

@@ -99,7 +99,7 @@ __device__ __forceinline__ bool reduce_exchange(const RedExchange& X, int64_t t,
 // part [G][RED_E], xpart [4][G][RED_E] floats, *xok_s.
 template <class A, int G, bool PRE, bool EX, bool LATE>
 __device__ __forceinline__ void reduce_body(const A& a, int bid, float* part, float* xpart, int* xok_ptr) {
-  static_assert(NREP % G == 0, "kinds 2-4: group pg takes replicas pg, pg + G, ...");
+  static_assert(NREP % G == 0 || G % NREP == 0, "kinds 2-4: group pg takes replicas pg, pg + G, ... (none when pg >= NREP)");
   static_assert(RED_E % 32 == 0, "kind 3 pairs lanes el and el + 16 of a 32-lane group");
   int& xok_s = *xok_ptr;  // EX: exchange live (no earlier timeout on this rank)
   auto PART = [&](int k, int e_) -> float& { return part[k * RED_E + e_]; };

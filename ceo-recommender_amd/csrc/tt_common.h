@@ -54,7 +54,19 @@ constexpr int FOLD_ROWS = 128;  // k_bwd_mid_fold row tile (8 waves)
 #define TT_FOLD_MIN_B 4096  // smallest batch that runs the folded BN0 backward (round 5: cfg 2 40.0 -> 38.9 us)
 #endif
 constexpr int LSR = 32;               // replica stride of the (dls, loss) pair
-__device__ __forceinline__ int rep_of_block() { return (int)(blockIdx.x % NREP); }
+// Replica of a block: (blockIdx.x / 8) % NREP spreads each XCD's blocks
+// (dispatched round robin: block b on XCD b % 8) over all NREP replicas;
+// blockIdx.x % NREP put all of an XCD's adds on one replica.  Three
+// interleaved rounds at cfg 3 (profiles/r06_rep_spread_ab): step 49.3-49.4 ->
+// 48.4-48.6 us (k_l0_fwd -0.5, k_l4_fwd -0.5 us); with the spread, 8 replicas
+// beat 4 (49.6) and 16 (49.3-49.4).  Placement changes speed only: any block
+// may add into any replica.
+#ifndef TT_REP_SPREAD
+#define TT_REP_SPREAD 1
+#endif
+__device__ __forceinline__ int rep_of_block() {
+  return TT_REP_SPREAD ? (int)((blockIdx.x >> 3) % NREP) : (int)(blockIdx.x % NREP);
+}
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

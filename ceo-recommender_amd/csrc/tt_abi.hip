@@ -151,8 +151,8 @@ static WsLayout make_ws(const Layout& L, int64_t max_batch) {
   int64_t off = 0;
   auto take = [&](int64_t n) { const int64_t o = off; off += round_up(n, 64); return o; };
   for (int t = 0; t < 2; ++t) {
-    W.st0[t] = take(NREP * 2 * H0);
-    W.st1[t] = take(NREP * 2 * H1);
+    W.st0[t] = take(NREP * ST0S);
+    W.st1[t] = take(NREP * ST1S);
     W.bng[t] = take(NREP * BNG);
     W.sh0[t] = take(H0);
     W.sh1[t] = take(H1);
@@ -568,9 +568,9 @@ static void red_step_fields(A& r, int part, const WsLayout& W, float* w, int64_t
   r.inv_b = 1.f / (float)n_rows;
   for (int t = 0; t < 2; ++t) {
     r.zero_buf[2 * t] = w + W.st0[t];
-    r.zero_len[2 * t] = part == RED_LATE ? 0 : NREP * 2 * H0;
+    r.zero_len[2 * t] = part == RED_LATE ? 0 : NREP * ST0S;
     r.zero_buf[2 * t + 1] = w + W.st1[t];
-    r.zero_len[2 * t + 1] = part == RED_EARLY ? 0 : NREP * 2 * H1;
+    r.zero_len[2 * t + 1] = part == RED_EARLY ? 0 : NREP * ST1S;
   }
   r.loss_state = state;
   if (apply_adam) {
@@ -935,8 +935,8 @@ static int32_t forward_impl(const tt_model_desc* d, const float* params, float* 
   a.emb = emb;
   if (train) {
     for (int t = 0; t < 2; ++t) {
-      (void)hipMemsetAsync(w + c.W.st0[t], 0, sizeof(float) * NREP * 2 * H0, s);
-      (void)hipMemsetAsync(w + c.W.st1[t], 0, sizeof(float) * NREP * 2 * H1, s);
+      (void)hipMemsetAsync(w + c.W.st0[t], 0, sizeof(float) * NREP * ST0S, s);
+      (void)hipMemsetAsync(w + c.W.st1[t], 0, sizeof(float) * NREP * ST1S, s);
     }
   }
   launch_l0(a, c.P, s);

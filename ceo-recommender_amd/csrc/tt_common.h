@@ -31,6 +31,13 @@ constexpr int MAX_KP = 256;  // padded tower input width supported by the fused 
 #define TT_NREP 8
 #endif
 constexpr int NREP = TT_NREP;
+// replica strides (floats) of the BN moment sums S1|S2 (st0: 2*64, st1: 2*32
+// floats of content); TT_REP_PAD spaces the replicas further apart
+#ifndef TT_REP_PAD
+#define TT_REP_PAD 0
+#endif
+constexpr int ST0S = 2 * H0 + TT_REP_PAD;
+constexpr int ST1S = 2 * H1 + TT_REP_PAD;
 constexpr int BNG = 2 * H0 + 2 * H1;  // one replica of a tower's BN-affine grads: gg0|gbe0|gg1|gbe1
 // Folded BN0 backward (k_bwd_mid<R, true>, numeric-only towers with kp <= 64):
 // one replica of a tower's fold sums: gg0 | gbe0 | sum Zhat0 | sum (X - shift)

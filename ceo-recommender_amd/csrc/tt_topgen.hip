@@ -51,7 +51,7 @@ __host__ __device__ constexpr size_t gen_bwd_lds(int D) {
 // statistics updated by block 0 when `update`; eval: the running statistics.
 __device__ __forceinline__ void gen_bn1_coefs(const StepArgs& a, const TowerDev& T, bool update, float* scratch,
                                               float* rst, float* cf) {
-  if (a.train) rep_sum<GEN_NTH, 2 * H1>(T.st1, 2 * H1, scratch, rst);
+  if (a.train) rep_sum<GEN_NTH, 2 * H1>(T.st1, ST1S, scratch, rst);
   if (threadIdx.x < H1) {
     const int c = threadIdx.x;
     const bool have_rs = T.rm1 != nullptr;

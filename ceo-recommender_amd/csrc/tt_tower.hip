@@ -544,7 +544,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L0) void k_l0_fwd(StepArgs a, 
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H0)
-      xblock_add(a.det, T.st0, 2 * H0, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<NW>(red, 2 * H0, threadIdx.x));
+      xblock_add(a.det, T.st0, ST0S, T.dslot, 2 * H0, threadIdx.x, wave_rows_sum<NW>(red, 2 * H0, threadIdx.x));
   }
   // the folded BN0 backward's replicas start every step at zero (k_bwd_mid
   // accumulates them, k_reduce_adam only reads them)
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
 #ifdef TT_DIAG_REP
   rs.issue(T.Z0 + (int64_t)(a.B / 2) * H0, 2 * H0);  // diagnostic (wrong values): plain-stored lines instead of the atomically built replicas
 #else
-  rs.issue(T.st0, 2 * H0);
+  rs.issue(T.st0, ST0S);
 #endif
   float bias[2];
 #pragma unroll
@@ -780,7 +780,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_L4) void k_l4_fwd(StepArgs a) 
   if (a.train) {
     __syncthreads();
     if (threadIdx.x < 2 * H1)
-      xblock_add(a.det, T.st1, 2 * H1, T.dslot, 2 * H1, threadIdx.x, wave_rows_sum<NW>(red, 2 * H1, threadIdx.x));
+      xblock_add(a.det, T.st1, ST1S, T.dslot, 2 * H1, threadIdx.x, wave_rows_sum<NW>(red, 2 * H1, threadIdx.x));
   }
   TT_STAMP(1, 7);
 }
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_TOP) void k_top(StepArgs a) {
     bn_be = pick(a.tw[0].be1, a.tw[1].be1)[bc];
   }
   RepSum2<NTH, 2 * H1> rs;
-  if (a.train) rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
+  if (a.train) rs.issue(a.tw[0].st1, a.tw[1].st1, ST1S);
   // while the replica loads are in flight: biases, zeroed partials, W8 images
   if (threadIdx.x < DP) {
     const bool ok = (int)threadIdx.x < D;
@@ -1348,7 +1348,7 @@ __global__ __launch_bounds__(R * 8) TT_WPE(TT_WPE_TOP) void k_top_pair(StepArgs 
     bn_be = pick(bt, a.tw[0].be1, a.tw[1].be1)[bc];
   }
   RepSum2<NTH, 2 * H1> rs;
-  rs.issue(a.tw[0].st1, a.tw[1].st1, 2 * H1);
+  rs.issue(a.tw[0].st1, a.tw[1].st1, ST1S);
   if (threadIdx.x < 2 * DP) smem[L::b8s + threadIdx.x] = (threadIdx.x % DP) < (unsigned)D ? b8v : 0.f;
 #pragma unroll
   for (int k = 0; k < WPT; ++k) {

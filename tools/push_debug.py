@@ -1,4 +1,4 @@
-"""Debug of the push exchange at world 2 on one GPU: one standalone launch,
+"""Debug of the push exchange (tools/push_debug.py N) at world 2 on one GPU: one standalone launch,
 then a dump of this rank's push rows (the words its peer stored)."""
 import ctypes
 import os
@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ceo-recommender_amd"))
 
 

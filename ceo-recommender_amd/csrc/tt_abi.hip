@@ -225,9 +225,18 @@ static void set_lds_attrs() {
                         (const void*)k_top_pair<4, 32>, (const void*)k_top_pair<8, 32>,
                         (const void*)k_bwd_mid<ROWS>, (const void*)k_bwd_mid_fold<FOLD_ROWS, true>,
                         (const void*)k_bwd_mid_fold<FOLD_ROWS, false>, (const void*)k_bwd_first<ROWS>};
-    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_top_gen_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_top_gen_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    // the dynamic limit is what the kernel's static LDS (e.g. a block vote's
+    // word) leaves of the CU's 160 KB; a refused attribute would otherwise
+    // stay behind as the thread's last error and fail the next launch check
+    auto set = [mx](const void* k) {
+      hipFuncAttributes fa;
+      const int st = hipFuncGetAttributes(&fa, k) == hipSuccess ? (int)fa.sharedSizeBytes : 0;
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx - st);
+    };
+    for (const void* k : ks) set(k);
+    set((const void*)k_top_gen_fwd);
+    set((const void*)k_top_gen_bwd);
+    (void)hipGetLastError();
   });
 }
 
@@ -1423,6 +1432,7 @@ static void nce_attrs() {
     for (const void* k : sim) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_SIM);
     for (const void* k : grad)
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_GRAD);
+    (void)hipGetLastError();  // (see set_lds_attrs)
   });
 }
 

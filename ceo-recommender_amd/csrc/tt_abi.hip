@@ -20,7 +20,7 @@
 
 #ifdef TT_STAMPS
 namespace tt {
-__device__ uint64_t* g_tt_stamps = nullptr;
+__constant__ uint64_t* g_tt_stamps = nullptr;  // __constant__: read with a scalar load, no vmcnt wait per stamp
 }
 extern "C" int32_t tt_debug_set_stamps(uint64_t* buf) {
   return (int32_t)hipMemcpyToSymbol(HIP_SYMBOL(tt::g_tt_stamps), &buf, sizeof(buf));

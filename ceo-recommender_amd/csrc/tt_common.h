@@ -551,7 +551,7 @@ __device__ __forceinline__ void xblock_add(bool det, float* rep, int rep_stride,
 #endif
 
 #ifdef TT_STAMPS
-extern __device__ uint64_t* g_tt_stamps;
+extern __constant__ uint64_t* g_tt_stamps;
 #define TT_STAMP_T(kid, slot, thr)                                                                      \
   do {                                                                                                  \
     if (g_tt_stamps && threadIdx.x == (thr))                                                            \
@@ -562,6 +562,13 @@ extern __device__ uint64_t* g_tt_stamps;
 #else
 #define TT_STAMP_T(kid, slot, thr) ((void)0)
 #define TT_STAMP(kid, slot) ((void)0)
+#endif
+// finer stamps inside one kernel's phases (kernel ids 6, 7), a separate
+// diagnostic build: -DTT_STAMPS -DTT_SUBSTAMPS
+#ifdef TT_SUBSTAMPS
+#define TT_SUBSTAMP(kid, slot) TT_STAMP(kid, slot)
+#else
+#define TT_SUBSTAMP(kid, slot) ((void)0)
 #endif
 
 __device__ __forceinline__ int64_t step_for_first_kernel(const StepArgs& a) {

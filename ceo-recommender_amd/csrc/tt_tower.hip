@@ -1918,6 +1918,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
   __syncthreads();
   TT_STAMP(3, 1);
   TT_STAMP_T(4, 1, 448);
+  TT_SUBSTAMP(6, 0);
 
   // ---- phase 1: X' gather issued (used in phase 3: its latency hides
   // behind this phase's arithmetic), dZ4, A0 / Zh0 recompute
@@ -1939,6 +1940,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
                           ld1(xrow[k], 4 * xc + 3));
     cv = make_float4(ld1(crow, 4 * xc), ld1(crow, 4 * xc + 1), ld1(crow, 4 * xc + 2), ld1(crow, 4 * xc + 3));
   }
+  TT_SUBSTAMP(6, 1);
 
   f32x4 dz[2];
 #pragma unroll
@@ -1959,6 +1961,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
     const float cb = col_reduce(dz[q][0] + dz[q][1] + dz[q][2] + dz[q][3]);
     if (g == 0) db4[w * H1 + col] = cb;
   }
+  TT_SUBSTAMP(6, 2);
   const bool drop = a.drop_thr > 0;
   const uint64_t key = dropout_key(a.seed, (uint64_t)step, t, 0);
   f32x4 a0[4], zh0[4];
@@ -1992,6 +1995,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
         kb |= ((h >> 16) >= a.drop_thr ? 1u : 0u) << (4 * (jp + 2) + i);
       }
   }
+  TT_SUBSTAMP(6, 3);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = 16 * j + r;
@@ -2008,9 +2012,11 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
     }
     put_planes4(hs + L::A0i + fold_at(col, 16 * w + 4 * g), L::PL, make_float4(a0[j][0], a0[j][1], a0[j][2], a0[j][3]));
   }
+  TT_SUBSTAMP(6, 4);
   __syncthreads();
   TT_STAMP(3, 2);
   TT_STAMP_T(4, 2, 448);
+  TT_SUBSTAMP(6, 5);
 
   // ---- phase 2: dW4 = dZ4^T A0 (wave w: h1-tile w & 1, h0-tile w >> 1),
   // dA0 = dZ4 W4 on the wave's rows -> dY0, BN0-backward column partials
@@ -2133,6 +2139,7 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
   __syncthreads();
   TT_STAMP(3, 6);
   TT_STAMP_T(4, 6, 448);
+  TT_SUBSTAMP(7, 0);
 
   // ---- phase 4: P | Q = [dY0 | Zh0]^T X' over the tile's rows (bf16x3,
   // K = rows in 32-row steps): wave w owns channels 16 (w & 3) .. +15 of P
@@ -2171,14 +2178,18 @@ __global__ __launch_bounds__(R * 4) TT_WPE(TT_WPE_MID) void k_bwd_mid_fold(StepA
         for (int j = 0; j < 4; ++j) acc[j] = mfma_bf16(af[kk & 1][PA[q]], bf[kk & 1][j][PB[q]], acc[j]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    TT_SUBSTAMP(7, 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (j < KT) store_tile_rm_wt(slab, so + 32 * j, 2 * kp, acc[j]);
   }
+  TT_SUBSTAMP(7, 2);
   static_assert(FRW == 4 * H0, "fold replica: gamma0 grad | beta0 grad | sum Zh0 | sum X'");
   if (threadIdx.x < 4 * H0)
     xblock_add(a.det, T.fr, FRW, T.dslot, FRW, threadIdx.x, wave_rows_sum<8>(red, 4 * H0, threadIdx.x));
+  TT_SUBSTAMP(7, 3);
   if (threadIdx.x < H1) slab[T.so_b4 + threadIdx.x] = wave_rows_sum<8>(db4, H1, threadIdx.x);
+  TT_SUBSTAMP(7, 4);
   TT_STAMP(3, 7);
   TT_STAMP_T(4, 7, 448);
 }

@@ -23,7 +23,8 @@ from bench import CONFIGS  # noqa: E402
 
 # kernel id 4: k_bwd_first on the six-kernel path; on the folded path (no
 # k_bwd_first) k_bwd_mid_fold stamps its wave 7 there (id 3 is its wave 0)
-NAMES = ["k_l0_fwd", "k_l4_fwd", "k_top", "k_bwd_mid", "k_bwd_first|mid_fold w7", "k_reduce_adam"]
+NAMES = ["k_l0_fwd", "k_l4_fwd", "k_top", "k_bwd_mid", "k_bwd_first|mid_fold w7", "k_reduce_adam",
+         "sub6", "sub7"]  # sub6 / sub7: TT_SUBSTAMPS builds (finer stamps inside one kernel)
 
 
 def main():
@@ -49,7 +50,7 @@ def main():
     tr.set_data(data)
     rows = torch.randperm(n, device=dev)
     nb = n // B
-    buf = torch.zeros(6 * 2048 * 8, dtype=torch.int64, device=dev)
+    buf = torch.zeros(8 * 2048 * 8, dtype=torch.int64, device=dev)
     for _ in range(5):
         tr.step_cycle(rows, B, nb)
     torch.cuda.synchronize()
@@ -59,11 +60,11 @@ def main():
         buf.zero_()
         tr.step_cycle(rows, B, nb)
         torch.cuda.synchronize()
-        st = buf.view(6, 2048, 8).cpu().numpy().astype(np.float64) / 100.0  # -> us
+        st = buf.view(8, 2048, 8).cpu().numpy().astype(np.float64) / 100.0  # -> us
         res[it] = st
     N.check(L.tt_debug_set_stamps(None), "set_stamps")
     st = res[4]
-    glob0 = min(st[k][st[k][:, 0] > 0, 0].min() for k in range(6) if (st[k][:, 0] > 0).any())
+    glob0 = min(st[k][st[k][:, 0] > 0, 0].min() for k in range(8) if (st[k][:, 0] > 0).any())
     for k, name in enumerate(NAMES):
         s = st[k]
         m = s[:, 0] > 0

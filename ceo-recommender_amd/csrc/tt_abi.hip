@@ -228,7 +228,7 @@ static void set_lds_attrs() {
     // the dynamic limit is what the kernel's static LDS (e.g. a block vote's
     // word) leaves of the CU's 160 KB; a refused attribute would otherwise
     // stay behind as the thread's last error and fail the next launch check
-    auto set = [mx](const void* k) {
+    auto set = [](const void* k) {
       hipFuncAttributes fa;
       const int st = hipFuncGetAttributes(&fa, k) == hipSuccess ? (int)fa.sharedSizeBytes : 0;
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx - st);

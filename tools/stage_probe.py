@@ -14,7 +14,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "ceo-recommender_amd"))
 
 B = 16384
-hip = ctypes.CDLL("libamdhip64.so")
+# the HIP runtime this process already uses (torch's bundled copy, which the
+# library binds to by soname): a bare "libamdhip64.so" could load a second one
+_tl = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+hip = ctypes.CDLL(_tl if os.path.exists(_tl) else "libamdhip64.so")
 hip.hipGetLastError.restype = ctypes.c_int
 
 
